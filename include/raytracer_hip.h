@@ -1,0 +1,203 @@
+/*
+ * raytracer_hip.h -- C ABI of libraytracer_hip, the MI355X (gfx950) drop-in for the
+ * per-pixel Whitted trace of TobiasDeBruijn/UU-INFOGR-Raytracer.
+ *
+ * The reference has no FFI: its plugin surface is the C# class
+ *   RayTracer(Surface screen)          Raytracer/RayTracer.cs:535-537
+ *   public readonly Surface screen     Raytracer/RayTracer.cs:506
+ *   public void Tick()                 Raytracer/RayTracer.cs:886-935
+ *   OnKeyPress(KeyboardKeyEventArgs)   Raytracer/RayTracer.cs:543-554
+ *   OnMouseMove(MouseMoveEventArgs)    Raytracer/RayTracer.cs:1058-1061
+ * plus Surface.width/height/int[] pixels (Raytracer/surface.cs:9-20).  Every entry
+ * point below replaces one piece of that surface; the C# P/Invoke shim that binds
+ * them is in INTEGRATION.md / shim/csharp/RayTracer.cs.
+ *
+ * Conventions
+ *  - Plain C, blittable POD structs of float32/int32 (no packing pragmas, no torch
+ *    types).  All functions return RT_OK (0) or a negative RT_ERR_* code and never
+ *    throw; rt_last_error() returns the message of the last failure.
+ *  - A context is used by one thread at a time (the reference calls Tick, OnKeyPress
+ *    and OnMouseMove from the GLFW render thread, template.cs:175-230).
+ *  - There is NO CPU fallback: rt_create fails with RT_ERR_NO_DEVICE when no gfx950
+ *    device is visible.
+ */
+#ifndef RAYTRACER_HIP_H
+#define RAYTRACER_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RT_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------------- */
+enum {
+    RT_OK = 0,
+    RT_ERR_INVALID_ARG = -1,   /* NULL pointer, negative size, bad enum value          */
+    RT_ERR_NO_DEVICE = -2,     /* no HIP device / not enough devices for n_gpus        */
+    RT_ERR_HIP = -3,           /* a HIP runtime call failed (message has the HIP text) */
+    RT_ERR_NO_SCENE = -4,      /* render before rt_set_scene                          */
+    RT_ERR_UNSUPPORTED = -5,   /* e.g. recursion_limit above RT_MAX_RECURSION_LIMIT    */
+    RT_ERR_RCCL = -6,          /* a RCCL call failed (multi-GPU contexts)              */
+    RT_ERR_OOM = -7            /* device allocation failed                            */
+};
+
+/* Deepest mirror chain the kernel's per-lane level stack holds: a limit of L
+ * shades levels 0..L (L+1 stack records).  The reference's own limit is 32
+ * (RayTracer.cs:490). */
+#define RT_MAX_RECURSION_LIMIT 63
+
+/* ---- scene description (RayTracer.cs:60-338, :441-469) ---------------------- */
+typedef struct rt_vec3 {
+    float x, y, z;
+} rt_vec3;
+
+/* Material, RayTracer.cs:60-110.  Flags are derived exactly as the reference does:
+ * IsMirror = km != 0, IsDiffuse = kd != 0, HasSpecularity = ks != 0 && n > 0
+ * (RayTracer.cs:85-93). */
+typedef struct rt_material {
+    rt_vec3 kd;  /* diffuseColor  K_d */
+    rt_vec3 ka;  /* ambientColor  K_a */
+    rt_vec3 ks;  /* specularColor K_s */
+    float n;     /* specularity   n   */
+    rt_vec3 km;  /* mirrorColor   K_m */
+} rt_material;
+
+/* Sphere, RayTracer.cs:308-338 (radiusSquared = radius*radius, :336). */
+typedef struct rt_sphere {
+    rt_vec3 center;
+    float radius;
+    rt_material material;
+} rt_sphere;
+
+/* Plane, RayTracer.cs:260-303.  Planes are always checkerboard-tiled: the
+ * reference's constructor ignores its isTiled argument (RayTracer.cs:289). */
+typedef struct rt_plane {
+    rt_vec3 center;
+    rt_vec3 normal;
+    rt_material material;
+} rt_plane;
+
+/* Light, RayTracer.cs:236-255. */
+typedef struct rt_light {
+    rt_vec3 position;
+    float intensity;
+} rt_light;
+
+/* Camera state of the reference: _cameraPosition, _yaw, _pitch (RayTracer.cs:494-502).
+ * The basis (RayTracer.cs:511-523) and view-plane size (RayTracer.cs:892-896) are
+ * derived from it once per frame on the host with the reference's double-precision
+ * trig (rt_camera_view). */
+typedef struct rt_camera {
+    rt_vec3 position;
+    float yaw;
+    float pitch;
+} rt_camera;
+
+/* Per-frame view derived from rt_camera and the surface size. */
+typedef struct rt_view {
+    rt_vec3 position;
+    rt_vec3 right;    /* CameraRightDirection   RayTracer.cs:517-518 */
+    rt_vec3 up;       /* CameraUpDirection      RayTracer.cs:522-523 */
+    rt_vec3 forward;  /* CameraForwardDirection RayTracer.cs:511-513 */
+    float plane_width, plane_height, near_clip;  /* viewParams RayTracer.cs:892-896 */
+} rt_view;
+
+/* Reference keys handled by OnKeyPress (RayTracer.cs:545-553). */
+enum {
+    RT_KEY_W = 1, RT_KEY_A = 2, RT_KEY_S = 3, RT_KEY_D = 4,
+    RT_KEY_SPACE = 5, RT_KEY_SHIFT = 6
+};
+
+/* Work counters of the visible (nearest-hit) path, accumulated since the last
+ * rt_reset_stats.  rays = primary + reflected segments (terminal segments included);
+ * shadow_rays = shaded diffuse hits x lights.  Times are device time measured with
+ * HIP events on the stream the kernel runs on. */
+typedef struct rt_stats {
+    uint64_t frames;
+    uint64_t pixels;
+    uint64_t primary_rays;
+    uint64_t reflect_rays;
+    uint64_t shadow_rays;
+    uint64_t sphere_tests;   /* algorithmic: (primary+reflect+shadow) x S */
+    uint64_t plane_tests;    /* algorithmic: (primary+reflect) x P        */
+    uint64_t launches;
+    double kernel_ms;        /* sum of trace-kernel durations            */
+    double last_kernel_ms;
+    double copy_ms;          /* sum of D2H / reassembly copy durations    */
+    double gather_ms;        /* sum of RCCL gather durations (multi-GPU)  */
+} rt_stats;
+
+typedef struct rt_ctx rt_ctx;
+
+/* ---- library / device ------------------------------------------------------- */
+int rt_abi_version(void);
+/* Number of visible HIP devices (0 when none).  Returns RT_OK or RT_ERR_HIP. */
+int rt_device_count(int* out_count);
+/* Message of the last failure on ctx (ctx may be NULL: last failure of this thread). */
+const char* rt_last_error(const rt_ctx* ctx);
+
+/* ---- context lifetime  (replaces `new RayTracer(screen)`, RayTracer.cs:535) ---- */
+/* n_gpus >= 1.  n_gpus > 1 creates one HIP stream per device and a single-process
+ * RCCL communicator (ncclCommInitAll); frames are split into interleaved row bands and
+ * gathered to device 0. */
+int rt_create(int n_gpus, rt_ctx** out_ctx);
+void rt_destroy(rt_ctx* ctx);
+
+/* ---- scene (replaces the hard-coded fields RayTracer.cs:441-490) ------------- */
+int rt_set_scene(rt_ctx* ctx,
+                 const rt_sphere* spheres, int n_spheres,
+                 const rt_plane* planes, int n_planes,
+                 const rt_light* lights, int n_lights,
+                 rt_vec3 ambient, int recursion_limit);
+
+/* ---- camera (mirrors RayTracer.cs:511-523, :543-554, :892-896, :1058-1061) ---- */
+int rt_set_camera(rt_ctx* ctx, const rt_camera* camera);
+int rt_get_camera(const rt_ctx* ctx, rt_camera* camera);
+int rt_camera_view(const rt_camera* camera, int width, int height, rt_view* out_view);
+int rt_camera_on_key(rt_camera* camera, int key);
+int rt_camera_on_mouse_move(rt_camera* camera, float delta_x, float delta_y);
+
+/* ---- rendering (replaces Tick(), RayTracer.cs:886-935) ---------------------- */
+/* Tick(): renders the full frame and copies it into the caller-owned host buffer
+ * pixels[width*height] (Surface.pixels, 0x00RRGGBB, row-major y*width+x).
+ * Synchronous: the pixels are complete on return, as template.cs:189-193 requires. */
+int rt_render(rt_ctx* ctx, int width, int height, int32_t* pixels);
+
+/* Pin a caller-owned host buffer (hipHostRegister) so rt_render's D2H copy lands
+ * directly in it; the shim registers Surface.pixels once. */
+int rt_register_host(rt_ctx* ctx, void* host_ptr, size_t bytes);
+int rt_unregister_host(rt_ctx* ctx, void* host_ptr);
+
+/* Device-resident variant (single-GPU contexts): renders the frame into
+ * d_pixels[width*height] on `hip_stream` (a hipStream_t, NULL = the context's own
+ * stream) and returns without synchronising. */
+int rt_render_device(rt_ctx* ctx, int width, int height, int32_t* d_pixels, void* hip_stream);
+
+/* Row-band shard (one process per GPU): renders the bands b = band_first,
+ * band_first+band_step, ... of band_rows rows each (rows [b*band_rows, (b+1)*band_rows)
+ * clipped to height) into d_out, packed band after band, each band width*band_rows
+ * int32 (rows past the image are left untouched).  Returns the number of bands in
+ * *out_n_bands when not NULL.  Asynchronous on hip_stream. */
+int rt_render_bands(rt_ctx* ctx, int width, int height, int band_rows, int band_first,
+                    int band_step, int32_t* d_out, void* hip_stream, int* out_n_bands);
+
+/* Reassemble: copies n_bands packed bands (as written by rt_render_bands with the same
+ * band_first/band_step) from d_bands into the row-major frame d_frame[width*height].
+ * Asynchronous on hip_stream. */
+int rt_scatter_bands(rt_ctx* ctx, int width, int height, int band_rows, int band_first,
+                     int band_step, const int32_t* d_bands, int32_t* d_frame, void* hip_stream);
+
+/* ---- statistics ------------------------------------------------------------- */
+/* Synchronises the context's pending work, then returns the counters. */
+int rt_get_stats(rt_ctx* ctx, rt_stats* out_stats);
+int rt_reset_stats(rt_ctx* ctx);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* RAYTRACER_HIP_H */

@@ -1,0 +1,85 @@
+"""ctypes wrapper of oracle/liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+Importable only from tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg,
+as the checker / the timed CPU baseline.  PARITY UNPINNED by the reference (see
+oracle/oracle.h).
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+
+MODE_REFERENCE = 0
+MODE_NEAREST = 1
+
+
+class OracleStats(C.Structure):
+    _fields_ = [("pixels", C.c_uint64), ("primary_rays", C.c_uint64), ("reflect_rays", C.c_uint64),
+                ("shadow_rays", C.c_uint64)]
+
+    def as_dict(self):
+        return {n: getattr(self, n) for n, _ in self._fields_}
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        import sys
+        sys.path.insert(0, os.path.join(os.path.dirname(HERE), "uu-infogr-raytracer_amd"))
+        from raytracer_hip import abi  # noqa: E402  (struct definitions only)
+        l = C.CDLL(LIB)
+        l.oracle_render.restype = C.c_int
+        l.oracle_render.argtypes = [C.POINTER(abi.rt_sphere), C.c_int, C.POINTER(abi.rt_plane), C.c_int,
+                                    C.POINTER(abi.rt_light), C.c_int, abi.rt_vec3, C.c_int,
+                                    C.POINTER(abi.rt_camera), C.c_int, C.c_int, C.c_int, C.c_int,
+                                    C.c_void_p, C.c_int, C.c_int, C.POINTER(OracleStats)]
+        l.oracle_intersect_sphere.restype = C.c_float
+        l.oracle_intersect_sphere.argtypes = [abi.rt_vec3, abi.rt_vec3, abi.rt_vec3, C.c_float, C.c_float,
+                                              C.POINTER(C.c_int)]
+        l.oracle_intersect_plane.restype = C.c_float
+        l.oracle_intersect_plane.argtypes = [abi.rt_vec3, abi.rt_vec3, abi.rt_vec3, abi.rt_vec3,
+                                             C.POINTER(C.c_int)]
+        l.oracle_shift_color.restype = C.c_int32
+        l.oracle_shift_color.argtypes = [abi.rt_vec3]
+        l.oracle_camera_view.restype = C.c_int
+        l.oracle_camera_view.argtypes = [C.POINTER(abi.rt_camera), C.c_int, C.c_int, C.POINTER(abi.rt_view)]
+        l.oracle_net_float_to_int.restype = C.c_int32
+        l.oracle_net_float_to_int.argtypes = [C.c_float]
+        l.abi = abi
+        _lib = l
+    return _lib
+
+
+def render(scene, mode=MODE_NEAREST, nthreads=None, rows=None, width=None, height=None):
+    """Render `scene` (raytracer_hip.scenes.Scene).  Returns (pixels[h_rows, W] int32, stats dict)."""
+    l = lib()
+    W = width or scene.width
+    H = height or scene.height
+    r0, r1 = rows if rows is not None else (0, H)
+    if nthreads is None:
+        nthreads = min(16, os.cpu_count() or 1)
+    S, P, L = scene.c_arrays()
+    cam = scene.c_camera()
+    out = np.zeros((r1 - r0, W), dtype=np.int32)
+    st = OracleStats()
+    rc = l.oracle_render(S, len(scene.spheres), P, len(scene.planes), L, len(scene.lights),
+                         l.abi.rt_vec3(*scene.ambient), scene.recursion_limit, C.byref(cam), W, H, r0, r1,
+                         out.ctypes.data, mode, nthreads, C.byref(st))
+    if rc != 0:
+        raise RuntimeError(f"oracle_render failed: {rc}")
+    return out, st.as_dict()

@@ -1,0 +1,80 @@
+"""Generate tests/golden/ fixtures from the CPU oracle (oracle/liboracle.so).
+
+The reference (C#/.NET 6 + OpenTK) ships no tests or golden images and cannot run in this
+image, so the fixtures are produced by the oracle and cross-validated here, before being
+written, by (1) the oracle's two independent drivers (all-hit reference-faithful vs
+nearest-only) on every case, and (2) the independent numpy float32 emulation
+(tests/emu_f32.py) on the small raw frames.
+
+    python tests/golden/make_golden.py          # rewrites golden.json and frames_*.npy
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+import zlib
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+sys.path.insert(0, os.path.join(ROOT, "uu-infogr-raytracer_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+import emu_f32  # noqa: E402
+import pyoracle  # noqa: E402
+from raytracer_hip import scenes  # noqa: E402
+
+# (case id, config, width, height): full-size frames -> CRC32 + ray counts
+CRC_CASES = [
+    ("REF_512", "REF", 512, 512),
+    ("REF_1280x720", "REF720", 1280, 720),
+    ("C1", "C1", 512, 512),
+    ("C2", "C2", 1920, 1080),
+    ("C3", "C3", 1920, 1080),
+    ("C4", "C4", 3840, 2160),
+    ("C5", "C5", 7680, 4320),
+]
+# small frames stored raw (and checked against the numpy emulation)
+RAW_CASES = [
+    ("REF_64", "REF", 64, 64),
+    ("REF_128", "REF", 128, 128),
+    ("C1_64", "C1", 64, 64),
+    ("C2_96x54", "C2", 96, 54),
+    ("C3_96x54", "C3", 96, 54),
+    ("C4_64x36", "C4", 64, 36),
+]
+REFERENCE_MODE_MAX_PIXELS = 4_000_000  # all-hit driver cross-check up to C3-size frames
+
+
+def crc(a: np.ndarray) -> str:
+    return f"{zlib.crc32(np.ascontiguousarray(a, dtype=np.int32).tobytes()) & 0xFFFFFFFF:08x}"
+
+
+def main():
+    nthreads = min(16, os.cpu_count() or 1)
+    out = {"generator": "oracle/liboracle.so (nearest-hit driver)", "cases": {}}
+    for cid, cfg, w, h in CRC_CASES + RAW_CASES:
+        sc = scenes.config(cfg).resized(w, h)
+        px, st = pyoracle.render(sc, pyoracle.MODE_NEAREST, nthreads)
+        if w * h <= REFERENCE_MODE_MAX_PIXELS:
+            ref, _ = pyoracle.render(sc, pyoracle.MODE_REFERENCE, nthreads)
+            assert np.array_equal(ref, px), f"{cid}: all-hit vs nearest drivers differ"
+        entry = {"config": cfg, "width": w, "height": h, "crc32": crc(px), "stats": st,
+                 "black_fraction": float((px == 0).mean())}
+        if (cid, cfg, w, h) in RAW_CASES:
+            emu = emu_f32.Emu(sc).render()
+            assert np.array_equal(emu, px), f"{cid}: numpy emulation differs from oracle"
+            fn = f"frame_{cid}.npy"
+            np.save(os.path.join(HERE, fn), px)
+            entry["frame"] = fn
+        out["cases"][cid] = entry
+        print(cid, entry["crc32"], st, flush=True)
+    with open(os.path.join(HERE, "golden.json"), "w") as f:
+        json.dump(out, f, indent=1, sort_keys=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,156 @@
+"""The C-ABI library: builds, loads, exports every entry point include/raytracer_hip.h
+declares, host-only helpers (camera math) match the oracle, and -- with no GPU in this
+container -- context creation fails loudly instead of falling back to the CPU."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from raytracer_hip import abi, scenes
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "raytracer_hip.h")
+
+
+def declared_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    names = re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\s*\*?\s*(rt_[a-z_0-9]+)\s*\(", src, flags=re.M)
+    return sorted(set(names))
+
+
+def test_header_declares_expected_api():
+    names = declared_functions()
+    assert len(names) == len(abi.EXPORTS), names
+    assert set(names) == {n for n, _, _ in abi.EXPORTS}
+
+
+def test_library_exports_every_declared_symbol(rtlib):
+    out = subprocess.run(["nm", "-D", "--defined-only", abi.LIB_PATH], capture_output=True, text=True,
+                         check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    missing = [n for n in declared_functions() if n not in exported]
+    assert not missing, missing
+    for n in declared_functions():
+        assert getattr(rtlib, n) is not None
+
+
+def test_library_is_gfx950_code_object(rtlib):
+    """The .so embeds a gfx950 code object (hipcc --offload-arch=gfx950) and nothing else."""
+    blob = open(abi.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    assert b"gfx942" not in blob and b"sm_" + b"90" not in blob
+
+
+def test_struct_layouts_match_header():
+    assert C.sizeof(abi.rt_vec3) == 12
+    assert C.sizeof(abi.rt_material) == 52   # C# Material is 52 B as well (RayTracer.cs:60-80)
+    assert C.sizeof(abi.rt_sphere) == 68
+    assert C.sizeof(abi.rt_plane) == 76
+    assert C.sizeof(abi.rt_light) == 16
+    assert C.sizeof(abi.rt_camera) == 20
+    assert C.sizeof(abi.rt_stats) == 8 * 8 + 4 * 8
+
+
+def test_abi_version(rtlib):
+    assert rtlib.rt_abi_version() == 1
+
+
+def test_camera_view_matches_oracle(rtlib, oracle):
+    ol = oracle.lib()
+    for cam in [abi.rt_camera(abi.rt_vec3(0, 0, 0), 0.0, 0.0),
+                abi.rt_camera(abi.rt_vec3(1.5, -0.25, 3.0), 0.7, -0.3),
+                abi.rt_camera(abi.rt_vec3(0, 0, 0), -2.9, 1.4)]:
+        for (w, h) in [(512, 512), (1920, 1080), (7, 3)]:
+            a, b = abi.rt_view(), abi.rt_view()
+            assert rtlib.rt_camera_view(C.byref(cam), w, h, C.byref(a)) == 0
+            assert ol.oracle_camera_view(C.byref(cam), w, h, C.byref(b)) == 0
+            assert bytes(a) == bytes(b)
+
+
+def _basis(cam):
+    """CameraForward/Right/Up restated in numpy (RayTracer.cs:511-523)."""
+    import math
+    f32 = np.float32
+    p, y = float(cam.pitch), float(cam.yaw)
+    F = np.array([math.cos(p) * math.sin(y), -math.sin(p), math.cos(p) * math.cos(y)]).astype(f32)
+    R = np.array([math.cos(y), 0.0, -math.sin(y)]).astype(f32)
+    U = np.array([R[1] * F[2] - R[2] * F[1], R[2] * F[0] - R[0] * F[2], R[0] * F[1] - R[1] * F[0]], dtype=f32)
+    return F, R, U
+
+
+def test_on_key_press_semantics(rtlib):
+    """OnKeyPress, RayTracer.cs:543-554: W/S along forward, A/D along right, Space/Shift along up."""
+    f32 = np.float32
+    cam = abi.rt_camera(abi.rt_vec3(0.5, 0.25, -1.0), 0.4, -0.2)
+    for key, which, sign in [(abi.RT_KEY_W, 0, 1), (abi.RT_KEY_S, 0, -1), (abi.RT_KEY_A, 1, -1),
+                             (abi.RT_KEY_D, 1, 1), (abi.RT_KEY_SPACE, 2, -1), (abi.RT_KEY_SHIFT, 2, 1)]:
+        c = abi.rt_camera.from_buffer_copy(cam)
+        pos = np.array(c.position.tuple(), dtype=f32)
+        d = _basis(c)[which] * f32(0.05)
+        want = pos + d if sign > 0 else pos - d
+        assert rtlib.rt_camera_on_key(C.byref(c), key) == 0
+        assert np.array_equal(np.array(c.position.tuple(), dtype=f32), want)
+    c = abi.rt_camera.from_buffer_copy(cam)
+    assert rtlib.rt_camera_on_key(C.byref(c), 99) == 0 and bytes(c) == bytes(cam)  # `_ => _cameraPosition`
+
+
+def test_on_mouse_move_semantics(rtlib):
+    f32 = np.float32
+    c = abi.rt_camera(abi.rt_vec3(0, 0, 0), 0.1, -0.2)
+    assert rtlib.rt_camera_on_mouse_move(C.byref(c), 7.0, -3.5) == 0
+    assert c.yaw == float(f32(0.1) + f32(7.0) / f32(360))
+    assert c.pitch == float(f32(-0.2) + f32(-3.5) / f32(360))
+
+
+def test_null_arguments_are_errors(rtlib):
+    assert rtlib.rt_camera_view(None, 4, 4, None) == abi.RT_ERR_INVALID_ARG
+    assert rtlib.rt_last_error(None)
+    assert rtlib.rt_set_scene(None, None, 0, None, 0, None, 0, abi.rt_vec3(0, 0, 0), 0) == abi.RT_ERR_INVALID_ARG
+    assert rtlib.rt_render(None, 4, 4, None) == abi.RT_ERR_INVALID_ARG
+    assert rtlib.rt_create(0, C.byref(C.c_void_p())) == abi.RT_ERR_INVALID_ARG
+
+
+def test_no_cpu_fallback_without_gpu(rtlib):
+    """In this GPU-less container rt_create must fail with RT_ERR_NO_DEVICE, not render on the CPU."""
+    n = C.c_int(-1)
+    assert rtlib.rt_device_count(C.byref(n)) == 0
+    if n.value > 0:
+        pytest.skip("a GPU is visible")
+    p = C.c_void_p()
+    assert rtlib.rt_create(1, C.byref(p)) == abi.RT_ERR_NO_DEVICE
+    assert b"no HIP device" in rtlib.rt_last_error(None)
+    from raytracer_hip import RayTracer, RayTracerError, Surface
+    with pytest.raises(RayTracerError):
+        RayTracer(Surface(8, 8))
+
+
+def test_scene_generator_deterministic():
+    a = scenes.config("C4")
+    b = scenes.config("C4")
+    assert a.spheres == b.spheres and len(a.spheres) == 64 and len(a.planes) == 2 and len(a.lights) == 4
+    c2 = scenes.config("C2")
+    assert c2.spheres == a.spheres[:8]
+    assert scenes.config("C3").recursion_limit == 3 and scenes.config("C5").width == 7680
+    for s in a.spheres[3:]:
+        for v in s.center + (s.radius,):
+            assert v * 64 == int(v * 64)  # quantised to 1/64
+    # SplitMix64 known answers (seed 0): the generator is the published algorithm
+    sm = scenes.SplitMix64(0)
+    assert sm.next() == 0xE220A8397B1DCDAF
+    assert sm.next() == 0x6E789E6AA1B965F4
+
+
+def test_reference_scene_verbatim():
+    sc = scenes.reference()
+    assert sc.recursion_limit == 32
+    assert sc.ambient[0] == float(np.float32(43) / np.float32(255))
+    red, green, mirror = sc.spheres
+    assert red.center == (2.5, 0.0, 8.0) and red.material.kd == (1.0, 0.0, 0.0) and red.material.ks == (0, 0, 0)
+    assert green.material.ks == (float(np.float32(0.4)),) * 3 and green.material.n == 1.0
+    assert mirror.material.km == (1.0, 1.0, 1.0) and mirror.material.kd == (0, 0, 0)
+    pl = sc.planes[0]
+    assert pl.material.n == 0.5 and pl.material.km == (1.0, 1.0, 1.0) and pl.material.ka == (0.5, 0.5, 0.5)

@@ -1,0 +1,202 @@
+"""GPU parity: libraytracer_hip (HIP, gfx950) against the CPU oracle, bit-exact int32 pixels
+and identical ray counts.  Every call goes through the C ABI.
+
+Bar: bit-exact for every pixel (integer packing of float colours whose computation is
+restated operation by operation) and identical visible-path ray counts.
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+from raytracer_hip import Context, RayTracer, Surface, abi, bands_of, scenes
+
+pytestmark = pytest.mark.gpu
+
+
+def crc(a):
+    return f"{zlib.crc32(np.ascontiguousarray(a, dtype=np.int32).tobytes()) & 0xFFFFFFFF:08x}"
+
+
+def ray_counts(st):
+    return {k: st[k] for k in ("primary_rays", "reflect_rays", "shadow_rays")}
+
+
+def render_gpu(ctx, sc):
+    ctx.set_scene(sc)
+    ctx.reset_stats()
+    px = ctx.render(sc.width, sc.height).copy()
+    return px, ctx.stats()
+
+
+def assert_same(px, want, what):
+    bad = px != want
+    if bad.any():
+        ys, xs = np.nonzero(bad)
+        pytest.fail(f"{what}: {int(bad.sum())} of {bad.size} pixels differ; first at (x={xs[0]}, y={ys[0]}): "
+                    f"gpu {px[ys[0], xs[0]]:#08x} oracle {want[ys[0], xs[0]]:#08x}")
+
+
+@pytest.mark.parametrize("cid", ["REF_64", "REF_128", "C1_64", "C2_96x54", "C3_96x54", "C4_64x36"])
+def test_small_frames_vs_committed_golden(gpu_ctx, golden, cid):
+    import os
+    e = golden["cases"][cid]
+    sc = scenes.config(e["config"]).resized(e["width"], e["height"])
+    px, st = render_gpu(gpu_ctx, sc)
+    want = np.load(os.path.join(os.path.dirname(__file__), "golden", e["frame"]))
+    assert_same(px, want, cid)
+    assert ray_counts(st) == {k: e["stats"][k] for k in ("primary_rays", "reflect_rays", "shadow_rays")}
+
+
+@pytest.mark.parametrize("cid", ["REF_512", "REF_1280x720", "C1", "C2", "C3", "C4", "C5"])
+def test_full_size_frames_vs_golden_and_oracle(gpu_ctx, golden, oracle, cid):
+    """BASELINE.json configs at their full sizes (C5 = 7680x4320, 33 Mpixel)."""
+    e = golden["cases"][cid]
+    sc = scenes.config(e["config"]).resized(e["width"], e["height"])
+    px, st = render_gpu(gpu_ctx, sc)
+    if crc(px) != e["crc32"]:
+        want, _ = oracle.render(sc, oracle.MODE_NEAREST)
+        assert_same(px, want, cid)
+    assert ray_counts(st) == {k: e["stats"][k] for k in ("primary_rays", "reflect_rays", "shadow_rays")}
+    assert st["pixels"] == e["width"] * e["height"]
+
+
+@pytest.mark.parametrize("seed", list(range(40)))
+def test_random_scenes_vs_oracle(gpu_ctx, oracle, seed):
+    import random_scenes
+    sc = random_scenes.random_scene(seed)
+    px, st = render_gpu(gpu_ctx, sc)
+    want, ost = oracle.render(sc, oracle.MODE_NEAREST, 4)
+    ref, _ = oracle.render(sc, oracle.MODE_REFERENCE, 4)
+    assert np.array_equal(want, ref)
+    assert_same(px, want, sc.name)
+    assert ray_counts(st) == {k: ost[k] for k in ("primary_rays", "reflect_rays", "shadow_rays")}
+
+
+@pytest.mark.parametrize("w,h", [(1, 1), (17, 13), (15, 16), (16, 15), (33, 65), (1000, 3)])
+def test_ragged_frame_sizes(gpu_ctx, oracle, w, h):
+    sc = scenes.config("C3").resized(w, h)
+    px, _ = render_gpu(gpu_ctx, sc)
+    want, _ = oracle.render(sc, oracle.MODE_NEAREST, 4)
+    assert_same(px, want, f"{w}x{h}")
+
+
+@pytest.mark.parametrize("limit", [0, 1, 2, 3, 4, 7, 8, 9, 32, 63])
+def test_recursion_limits_across_stack_variants(gpu_ctx, oracle, limit):
+    """K = 1/2/4/8 register stacks and the 64-deep scratch stack (limit+1 records)."""
+    sc = scenes.reference(160, 120)
+    sc.recursion_limit = limit
+    sc.camera = ((-1.5, -0.5, 4.0), -0.9, 0.1)  # looks at the mirror sphere over the mirror floor
+    px, st = render_gpu(gpu_ctx, sc)
+    want, ost = oracle.render(sc, oracle.MODE_NEAREST, 4)
+    assert_same(px, want, f"limit {limit}")
+    assert ray_counts(st) == {k: ost[k] for k in ("primary_rays", "reflect_rays", "shadow_rays")}
+
+
+def test_empty_scene_is_black(gpu_ctx):
+    sc = scenes.Scene("empty", 40, 30, [], [], [], scenes.REF_AMBIENT, 0)
+    px, st = render_gpu(gpu_ctx, sc)
+    assert (px == 0).all() and st["reflect_rays"] == 0 and st["shadow_rays"] == 0
+
+
+def test_no_lights_only_ambient_and_mirrors(gpu_ctx, oracle):
+    sc = scenes.reference(64, 64)
+    sc.lights = []
+    px, st = render_gpu(gpu_ctx, sc)
+    want, _ = oracle.render(sc, oracle.MODE_NEAREST, 4)
+    assert_same(px, want, "no lights")
+    assert st["shadow_rays"] == 0
+
+
+@pytest.mark.parametrize("band_rows,nranks", [(8, 2), (8, 3), (5, 8), (16, 1), (7, 5), (1, 4)])
+def test_row_bands_reassemble(gpu_ctx, band_rows, nranks):
+    """rt_render_bands on every band set + rt_scatter_bands == the full frame (the multi-GPU data path)."""
+    import torch
+    sc = scenes.config("C3").resized(200, 117)
+    gpu_ctx.set_scene(sc)
+    W, H = sc.width, sc.height
+    full = gpu_ctx.render(W, H).copy()
+    frame = torch.full((H * W,), -1, dtype=torch.int32, device="cuda")
+    stream = torch.cuda.current_stream().cuda_stream
+    for r in range(nranks):
+        nb = bands_of(H, band_rows, r, nranks)
+        buf = torch.full((max(1, nb) * band_rows * W,), -7, dtype=torch.int32, device="cuda")
+        got = gpu_ctx.render_bands(W, H, band_rows, r, nranks, buf.data_ptr(), stream)
+        assert got == nb
+        gpu_ctx.scatter_bands(W, H, band_rows, r, nranks, buf.data_ptr(), frame.data_ptr(), stream)
+    torch.cuda.synchronize()
+    assert np.array_equal(frame.cpu().numpy().reshape(H, W), full)
+
+
+def test_render_device_on_torch_stream(gpu_ctx, golden):
+    import torch
+    e = golden["cases"]["C2"]
+    sc = scenes.config("C2")
+    gpu_ctx.set_scene(sc)
+    out = torch.zeros(sc.width * sc.height, dtype=torch.int32, device="cuda")
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        gpu_ctx.render_device(sc.width, sc.height, out.data_ptr(), s.cuda_stream)
+    s.synchronize()
+    assert crc(out.cpu().numpy()) == e["crc32"]
+
+
+def test_reference_plugin_surface_tick_and_input(oracle):
+    """RayTracer(Surface).Tick()/OnKeyPress/OnMouseMove, as template.cs drives it."""
+    screen = Surface(128, 96)
+    rt = RayTracer(screen)
+    try:
+        rt.Tick()
+        want, _ = oracle.render(scenes.reference(128, 96), oracle.MODE_NEAREST, 4)
+        assert_same(screen.image(), want, "Tick default camera")
+        for key in ["W", "W", "A", "Space", "D", "LeftShift", "S", "Q"]:
+            rt.OnKeyPress(key)
+        rt.OnMouseMove(25.0, -12.0)
+        rt.OnKeyPress("W")
+        rt.Tick()
+        sc = scenes.reference(128, 96)
+        c = rt.camera
+        sc.camera = (c.position.tuple(), c.yaw, c.pitch)
+        want, _ = oracle.render(sc, oracle.MODE_NEAREST, 4)
+        assert_same(screen.image(), want, "Tick moved camera")
+    finally:
+        rt.close()
+
+
+def test_error_behaviour(rtlib):
+    import ctypes as C
+    ctx = Context(1)
+    try:
+        W = 16
+        buf = np.zeros(W * W, dtype=np.int32)
+        assert rtlib.rt_render(ctx.ptr, W, W, buf.ctypes.data) == abi.RT_ERR_NO_SCENE
+        sc = scenes.reference(W, W)
+        S, P, L = sc.c_arrays()
+        rc = rtlib.rt_set_scene(ctx.ptr, S, 3, P, 1, L, 2, abi.rt_vec3(0, 0, 0), abi.RT_MAX_RECURSION_LIMIT + 1)
+        assert rc == abi.RT_ERR_UNSUPPORTED and b"recursion_limit" in rtlib.rt_last_error(ctx.ptr)
+        assert rtlib.rt_set_scene(ctx.ptr, S, -1, P, 1, L, 2, abi.rt_vec3(0, 0, 0), 1) == abi.RT_ERR_INVALID_ARG
+        ctx.set_scene(sc)
+        assert rtlib.rt_render(ctx.ptr, 0, W, buf.ctypes.data) == abi.RT_ERR_INVALID_ARG
+        assert rtlib.rt_render(ctx.ptr, W, W, None) == abi.RT_ERR_INVALID_ARG
+    finally:
+        ctx.close()
+    n = C.c_int(0)
+    rtlib.rt_device_count(C.byref(n))
+    p = C.c_void_p()
+    assert rtlib.rt_create(n.value + 1, C.byref(p)) == abi.RT_ERR_NO_DEVICE
+
+
+def test_stats_accumulate_and_reset(gpu_ctx, golden):
+    e = golden["cases"]["C1"]
+    sc = scenes.config("C1")
+    gpu_ctx.set_scene(sc)
+    gpu_ctx.reset_stats()
+    for _ in range(3):
+        gpu_ctx.render(sc.width, sc.height)
+    st = gpu_ctx.stats()
+    assert st["frames"] == 3 and st["launches"] == 3
+    assert st["primary_rays"] == 3 * e["stats"]["primary_rays"]
+    assert st["sphere_tests"] == (st["primary_rays"] + st["reflect_rays"] + st["shadow_rays"]) * 3
+    assert st["kernel_ms"] > 0 and st["copy_ms"] > 0
+    gpu_ctx.reset_stats()
+    assert gpu_ctx.stats()["primary_rays"] == 0

@@ -1,0 +1,686 @@
+// rt_api.cpp -- C ABI of libraytracer_hip (include/raytracer_hip.h).
+//
+// Host side of the drop-in: context lifetime, scene upload (with the scene-constant
+// precomputation described in rt_internal.h), camera math (RayTracer.cs:511-523,
+// :543-554, :892-896, :1058-1061), frame rendering (single GPU, row bands, and a
+// single-process multi-GPU path that gathers row bands over RCCL), HIP-event timing
+// and work counters.  Never throws across the ABI; no CPU fallback.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <dlfcn.h>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/raytracer_hip.h"
+#include "rt_internal.h"
+
+using namespace rtk;
+
+// ----------------------------------------------------------------------------
+// minimal RCCL binding (resolved with dlopen only for multi-GPU contexts, so a
+// single-GPU process never needs librccl)
+// ----------------------------------------------------------------------------
+namespace {
+typedef void* ncclComm_t;
+typedef int ncclResult_t;
+enum { ncclInt32 = 2 };
+struct Rccl {
+    void* h = nullptr;
+    ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
+    ncclResult_t (*CommDestroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*Gather)(const void*, void*, size_t, int, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*GroupStart)() = nullptr;
+    ncclResult_t (*GroupEnd)() = nullptr;
+    const char* (*GetErrorString)(ncclResult_t) = nullptr;
+    bool load(std::string& err) {
+        if (h) return true;
+        const char* names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
+        for (const char* n : names)
+            if ((h = dlopen(n, RTLD_NOW | RTLD_GLOBAL))) break;
+        if (!h) {
+            err = "dlopen(librccl) failed";
+            return false;
+        }
+        CommInitAll = (decltype(CommInitAll))dlsym(h, "ncclCommInitAll");
+        CommDestroy = (decltype(CommDestroy))dlsym(h, "ncclCommDestroy");
+        Gather = (decltype(Gather))dlsym(h, "ncclGather");
+        GroupStart = (decltype(GroupStart))dlsym(h, "ncclGroupStart");
+        GroupEnd = (decltype(GroupEnd))dlsym(h, "ncclGroupEnd");
+        GetErrorString = (decltype(GetErrorString))dlsym(h, "ncclGetErrorString");
+        if (!CommInitAll || !CommDestroy || !Gather || !GroupStart || !GroupEnd) {
+            err = "librccl lacks ncclCommInitAll/ncclGather/ncclGroupStart";
+            return false;
+        }
+        return true;
+    }
+};
+Rccl g_rccl;
+
+thread_local std::string g_last_error;
+
+struct EventPair {
+    hipEvent_t a = nullptr, b = nullptr;
+    int kind = 0;  // 0 kernel, 1 copy, 2 gather
+};
+
+struct Device {
+    int id = 0;
+    hipStream_t stream = nullptr;
+    void* d_scene = nullptr;
+    size_t scene_cap = 0;
+    int32_t* d_frame = nullptr;  // full frame (device 0 of multi-GPU contexts)
+    size_t frame_cap = 0;
+    int32_t* d_bands = nullptr;  // this device's packed row bands (multi-GPU)
+    size_t bands_cap = 0;
+    int32_t* d_gather = nullptr;  // device 0: n_gpus x padded band sets
+    size_t gather_cap = 0;
+    unsigned long long* d_counters = nullptr;
+    std::vector<EventPair> pending, pool;
+    ncclComm_t comm = nullptr;
+};
+
+struct SceneLayout {
+    int S = 0, P = 0, L = 0, limit = 0;
+    size_t off_sph = 0, off_mat = 0, off_pl = 0, off_li = 0, bytes = 0;
+};
+}  // namespace
+
+struct rt_ctx {
+    int n_gpus = 1;
+    std::vector<Device> dev;
+    bool has_scene = false;
+    SceneLayout layout;
+    rt_camera cam{};
+    std::string last_error;
+    uint64_t frames = 0, pixels = 0, launches = 0;
+    double kernel_ms = 0, last_kernel_ms = 0, copy_ms = 0, gather_ms = 0;
+    int32_t* host_staging = nullptr;
+};
+
+// ----------------------------------------------------------------------------
+// error helpers
+// ----------------------------------------------------------------------------
+static int fail(rt_ctx* ctx, int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    if (ctx) ctx->last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(ctx, call)                                                                                 \
+    do {                                                                                                   \
+        hipError_t e_ = (call);                                                                            \
+        if (e_ != hipSuccess) return fail((ctx), RT_ERR_HIP, "%s failed: %s", #call, hipGetErrorString(e_)); \
+    } while (0)
+
+namespace {
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        if (prev != dev) (void)hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (prev >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+int grow(rt_ctx* ctx, void** p, size_t* cap, size_t bytes) {
+    if (*cap >= bytes) return RT_OK;
+    if (*p) (void)hipFree(*p);
+    *p = nullptr;
+    *cap = 0;
+    hipError_t e = hipMalloc(p, bytes);
+    if (e != hipSuccess) return fail(ctx, RT_ERR_OOM, "hipMalloc(%zu) failed: %s", bytes, hipGetErrorString(e));
+    *cap = bytes;
+    return RT_OK;
+}
+
+// Sum completed event pairs into the context totals (waits for them).
+void drain_events(rt_ctx* ctx, Device& d) {
+    for (EventPair& ep : d.pending) {
+        float ms = 0.0f;
+        (void)hipEventSynchronize(ep.b);
+        if (hipEventElapsedTime(&ms, ep.a, ep.b) == hipSuccess) {
+            if (ep.kind == 0) {
+                ctx->kernel_ms += ms;
+                ctx->last_kernel_ms = ms;
+            } else if (ep.kind == 1) {
+                ctx->copy_ms += ms;
+            } else {
+                ctx->gather_ms += ms;
+            }
+        }
+        d.pool.push_back(ep);
+    }
+    d.pending.clear();
+}
+
+EventPair* begin_timed(rt_ctx* ctx, Device& d, int kind) {
+    if (d.pending.size() >= 4096) drain_events(ctx, d);  // bound host memory; stalls only then
+    EventPair ep;
+    if (!d.pool.empty()) {
+        ep = d.pool.back();
+        d.pool.pop_back();
+    } else {
+        if (hipEventCreate(&ep.a) != hipSuccess || hipEventCreate(&ep.b) != hipSuccess) return nullptr;
+    }
+    ep.kind = kind;
+    (void)hipEventRecord(ep.a, d.stream);
+    d.pending.push_back(ep);
+    return &d.pending.back();
+}
+
+void end_timed(Device& d) { (void)hipEventRecord(d.pending.back().b, d.stream); }
+
+// Host-side Vector3 helpers (binary32, no contraction: built with -ffp-contract=off).
+struct H3 {
+    float x, y, z;
+};
+H3 h3(rt_vec3 v) { return H3{v.x, v.y, v.z}; }
+float hdot(H3 a, H3 b) { return ((a.x * b.x) + (a.y * b.y)) + (a.z * b.z); }
+H3 hcross(H3 l, H3 r) {
+    return H3{(l.y * r.z) - (l.z * r.y), (l.z * r.x) - (l.x * r.z), (l.x * r.y) - (l.y * r.x)};
+}
+H3 hnormalize(H3 a) {
+    float s = 1.0f / std::sqrt(hdot(a, a));
+    return H3{a.x * s, a.y * s, a.z * s};
+}
+bool hzero(rt_vec3 v) { return v.x == 0 && v.y == 0 && v.z == 0; }
+
+DevMaterial dev_material(const rt_material& m, rt_vec3 ambient) {
+    DevMaterial d;
+    std::memset(&d, 0, sizeof d);
+    d.kd[0] = m.kd.x, d.kd[1] = m.kd.y, d.kd[2] = m.kd.z;
+    d.amb[0] = ambient.x * m.ka.x, d.amb[1] = ambient.y * m.ka.y, d.amb[2] = ambient.z * m.ka.z;
+    d.ks[0] = m.ks.x, d.ks[1] = m.ks.y, d.ks[2] = m.ks.z;
+    d.n = m.n;
+    d.km[0] = m.km.x, d.km[1] = m.km.y, d.km[2] = m.km.z;
+    d.flags = (hzero(m.km) ? 0u : MAT_MIRROR) | (hzero(m.kd) ? 0u : MAT_DIFFUSE) |
+              ((!hzero(m.ks) && m.n > 0.0f) ? MAT_SPEC : 0u);
+    d.pow_kind = m.n == 1.0f ? POW_ONE : m.n == 0.5f ? POW_HALF : m.n == 2.0f ? POW_TWO : POW_GENERIC;
+    return d;
+}
+
+int total_bands(int H, int band_rows) { return (H + band_rows - 1) / band_rows; }
+int bands_of(int H, int band_rows, int first, int step) {
+    int tb = total_bands(H, band_rows);
+    return first < tb ? (tb - 1 - first) / step + 1 : 0;
+}
+
+int view_params(rt_ctx* ctx, int W, int H, LaunchParams& lp) {
+    rt_view v;
+    int rc = rt_camera_view(&ctx->cam, W, H, &v);
+    if (rc != RT_OK) return fail(ctx, rc, "invalid frame size %dx%d", W, H);
+    lp.cam[0] = v.position.x, lp.cam[1] = v.position.y, lp.cam[2] = v.position.z;
+    lp.right[0] = v.right.x, lp.right[1] = v.right.y, lp.right[2] = v.right.z;
+    lp.up[0] = v.up.x, lp.up[1] = v.up.y, lp.up[2] = v.up.z;
+    lp.fwd[0] = v.forward.x, lp.fwd[1] = v.forward.y, lp.fwd[2] = v.forward.z;
+    lp.pw = v.plane_width, lp.ph = v.plane_height, lp.nearc = v.near_clip;
+    lp.W = W, lp.H = H;
+    return RT_OK;
+}
+
+void scene_params(const rt_ctx* ctx, const Device& d, LaunchParams& lp) {
+    const SceneLayout& L = ctx->layout;
+    const char* base = (const char*)d.d_scene;
+    lp.sph = (const DevSphere*)(base + L.off_sph);
+    lp.mat = (const DevMaterial*)(base + L.off_mat);
+    lp.pl = (const DevPlane*)(base + L.off_pl);
+    lp.li = (const DevLight*)(base + L.off_li);
+    lp.S = L.S, lp.P = L.P, lp.L = L.L, lp.limit = L.limit;
+    lp.counters = d.d_counters;
+}
+
+// Launch the trace of bands (first, step) of `band_rows` rows into `out` on device d.
+int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int band_rows, int first, int step,
+                int32_t* out, int* n_bands) {
+    LaunchParams lp;
+    std::memset(&lp, 0, sizeof lp);
+    int rc = view_params(ctx, W, H, lp);
+    if (rc != RT_OK) return rc;
+    scene_params(ctx, d, lp);
+    const int nb = bands_of(H, band_rows, first, step);
+    if (n_bands) *n_bands = nb;
+    lp.band_rows = band_rows, lp.band_first = first, lp.band_step = step;
+    lp.local_rows = nb * band_rows;
+    lp.out = out;
+    hipStream_t saved = d.stream;
+    d.stream = stream;
+    begin_timed(ctx, d, 0);
+    int e = launch_trace(lp, stream);
+    end_timed(d);
+    d.stream = saved;
+    if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "trace launch failed: %s", hipGetErrorString((hipError_t)e));
+    ctx->launches++;
+    return RT_OK;
+}
+
+int check_ctx(rt_ctx* ctx, int W, int H) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "NULL context");
+    if (!ctx->has_scene) return fail(ctx, RT_ERR_NO_SCENE, "rt_set_scene has not been called");
+    if (W <= 0 || H <= 0 || (long long)W * H > (1LL << 31) - 1)
+        return fail(ctx, RT_ERR_INVALID_ARG, "invalid frame size %dx%d", W, H);
+    return RT_OK;
+}
+}  // namespace
+
+// ============================================================================
+// exported C ABI
+// ============================================================================
+extern "C" {
+
+int rt_abi_version(void) { return RT_ABI_VERSION; }
+
+int rt_device_count(int* out_count) {
+    if (!out_count) return fail(nullptr, RT_ERR_INVALID_ARG, "NULL out_count");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e == hipErrorNoDevice || e == hipErrorInvalidDevice) n = 0;
+    else if (e != hipSuccess) return fail(nullptr, RT_ERR_HIP, "hipGetDeviceCount: %s", hipGetErrorString(e));
+    *out_count = n;
+    return RT_OK;
+}
+
+const char* rt_last_error(const rt_ctx* ctx) {
+    if (ctx) return ctx->last_error.c_str();
+    return g_last_error.c_str();
+}
+
+int rt_create(int n_gpus, rt_ctx** out_ctx) {
+    if (!out_ctx || n_gpus < 1) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_create: bad arguments");
+    *out_ctx = nullptr;
+    int ndev = 0;
+    if (rt_device_count(&ndev) != RT_OK || ndev == 0)
+        return fail(nullptr, RT_ERR_NO_DEVICE, "no HIP device visible (libraytracer_hip has no CPU fallback)");
+    if (n_gpus > ndev) return fail(nullptr, RT_ERR_NO_DEVICE, "rt_create(%d): only %d devices visible", n_gpus, ndev);
+    rt_ctx* ctx = new (std::nothrow) rt_ctx();
+    if (!ctx) return fail(nullptr, RT_ERR_OOM, "out of host memory");
+    ctx->n_gpus = n_gpus;
+    ctx->dev.resize((size_t)n_gpus);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (int g = 0; g < n_gpus; ++g) {
+        Device& d = ctx->dev[(size_t)g];
+        d.id = n_gpus == 1 ? cur : g;  // single-GPU: the caller's current device
+        DeviceGuard guard(d.id);
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, d.id) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+            int rc = fail(ctx, RT_ERR_NO_DEVICE, "device %d is %s, this build targets gfx950", d.id, prop.gcnArchName);
+            g_last_error = ctx->last_error;
+            rt_destroy(ctx);
+            return rc;
+        }
+        hipError_t e = hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking);
+        if (e == hipSuccess) e = hipMalloc((void**)&d.d_counters, 4 * sizeof(unsigned long long));
+        if (e == hipSuccess) e = hipMemset(d.d_counters, 0, 4 * sizeof(unsigned long long));
+        if (e != hipSuccess) {
+            int rc = fail(ctx, RT_ERR_HIP, "device %d init: %s", d.id, hipGetErrorString(e));
+            g_last_error = ctx->last_error;
+            rt_destroy(ctx);
+            return rc;
+        }
+    }
+    if (n_gpus > 1) {
+        std::string err;
+        if (!g_rccl.load(err)) {
+            fail(ctx, RT_ERR_RCCL, "%s", err.c_str());
+            rt_destroy(ctx);
+            return RT_ERR_RCCL;
+        }
+        std::vector<ncclComm_t> comms((size_t)n_gpus);
+        std::vector<int> ids((size_t)n_gpus);
+        for (int g = 0; g < n_gpus; ++g) ids[(size_t)g] = ctx->dev[(size_t)g].id;
+        ncclResult_t r = g_rccl.CommInitAll(comms.data(), n_gpus, ids.data());
+        if (r != 0) {
+            fail(ctx, RT_ERR_RCCL, "ncclCommInitAll: %s", g_rccl.GetErrorString ? g_rccl.GetErrorString(r) : "?");
+            g_last_error = ctx->last_error;
+            rt_destroy(ctx);
+            return RT_ERR_RCCL;
+        }
+        for (int g = 0; g < n_gpus; ++g) ctx->dev[(size_t)g].comm = comms[(size_t)g];
+    }
+    *out_ctx = ctx;
+    return RT_OK;
+}
+
+void rt_destroy(rt_ctx* ctx) {
+    if (!ctx) return;
+    for (Device& d : ctx->dev) {
+        DeviceGuard guard(d.id);
+        if (d.stream) (void)hipStreamSynchronize(d.stream);
+        for (EventPair& ep : d.pending) (void)hipEventDestroy(ep.a), (void)hipEventDestroy(ep.b);
+        for (EventPair& ep : d.pool) (void)hipEventDestroy(ep.a), (void)hipEventDestroy(ep.b);
+        if (d.comm && g_rccl.CommDestroy) (void)g_rccl.CommDestroy(d.comm);
+        if (d.d_scene) (void)hipFree(d.d_scene);
+        if (d.d_frame) (void)hipFree(d.d_frame);
+        if (d.d_bands) (void)hipFree(d.d_bands);
+        if (d.d_gather) (void)hipFree(d.d_gather);
+        if (d.d_counters) (void)hipFree(d.d_counters);
+        if (d.stream) (void)hipStreamDestroy(d.stream);
+    }
+    delete ctx;
+}
+
+int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_plane* planes, int n_planes,
+                 const rt_light* lights, int n_lights, rt_vec3 ambient, int recursion_limit) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "NULL context");
+    if (n_spheres < 0 || n_planes < 0 || n_lights < 0 || (n_spheres && !spheres) || (n_planes && !planes) ||
+        (n_lights && !lights))
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_set_scene: bad primitive arrays");
+    if (recursion_limit < 0) return fail(ctx, RT_ERR_INVALID_ARG, "recursion_limit must be >= 0");
+    if (recursion_limit > RT_MAX_RECURSION_LIMIT)
+        return fail(ctx, RT_ERR_UNSUPPORTED, "recursion_limit %d > RT_MAX_RECURSION_LIMIT (%d)", recursion_limit,
+                    RT_MAX_RECURSION_LIMIT);
+
+    SceneLayout L;
+    L.S = n_spheres, L.P = n_planes, L.L = n_lights, L.limit = recursion_limit;
+    auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    L.off_sph = 0;
+    L.off_mat = al(L.off_sph + sizeof(DevSphere) * (size_t)n_spheres);
+    L.off_pl = al(L.off_mat + sizeof(DevMaterial) * (size_t)(n_spheres + n_planes));
+    L.off_li = al(L.off_pl + sizeof(DevPlane) * (size_t)n_planes);
+    L.bytes = al(L.off_li + sizeof(DevLight) * (size_t)n_lights) + 256;
+
+    std::vector<unsigned char> blob(L.bytes, 0);
+    DevSphere* sph = (DevSphere*)(blob.data() + L.off_sph);
+    DevMaterial* mat = (DevMaterial*)(blob.data() + L.off_mat);
+    DevPlane* pl = (DevPlane*)(blob.data() + L.off_pl);
+    DevLight* li = (DevLight*)(blob.data() + L.off_li);
+    for (int i = 0; i < n_spheres; ++i) {
+        const rt_sphere& s = spheres[i];
+        sph[i] = DevSphere{s.center.x, s.center.y, s.center.z, s.radius * s.radius};  // :336
+        mat[i] = dev_material(s.material, ambient);
+    }
+    for (int i = 0; i < n_planes; ++i) {
+        const rt_plane& p = planes[i];
+        const H3 n = h3(p.normal);
+        DevPlane d;
+        std::memset(&d, 0, sizeof d);
+        d.cx = p.center.x, d.cy = p.center.y, d.cz = p.center.z;
+        d.cn = hdot(h3(p.center), n);  // Vector3.Dot(plane.center, plane.normal), :594
+        d.nx = n.x, d.ny = n.y, d.nz = n.z;
+        H3 e1 = hnormalize(hcross(n, H3{1.0f, 0.0f, 0.0f}));  // :760-763
+        if (e1.x == 0 && e1.y == 0 && e1.z == 0) e1 = hnormalize(hcross(n, H3{0.0f, 0.0f, 1.0f}));
+        H3 e2 = hnormalize(hcross(n, e1));  // :765
+        d.e1x = e1.x, d.e1y = e1.y, d.e1z = e1.z;
+        d.e2x = e2.x, d.e2y = e2.y, d.e2z = e2.z;
+        pl[i] = d;
+        mat[n_spheres + i] = dev_material(p.material, ambient);
+    }
+    for (int i = 0; i < n_lights; ++i) {
+        const rt_light& l = lights[i];
+        const H3 p = h3(l.position);
+        DevLight d;
+        std::memset(&d, 0, sizeof d);
+        d.px = p.x, d.py = p.y, d.pz = p.z, d.intensity = l.intensity;
+        d.a = hdot(p, p);  // IntersectsSphere's a = Dot(direction, direction), :617
+        d.a2 = 2.0f * d.a;
+        d.a4 = 4.0f * d.a;
+        li[i] = d;
+    }
+    for (Device& d : ctx->dev) {
+        DeviceGuard guard(d.id);
+        HIP_TRY(ctx, hipStreamSynchronize(d.stream));
+        int rc = grow(ctx, &d.d_scene, &d.scene_cap, L.bytes);
+        if (rc != RT_OK) return rc;
+        HIP_TRY(ctx, hipMemcpy(d.d_scene, blob.data(), L.bytes, hipMemcpyHostToDevice));
+    }
+    ctx->layout = L;
+    ctx->has_scene = true;
+    return RT_OK;
+}
+
+int rt_set_camera(rt_ctx* ctx, const rt_camera* camera) {
+    if (!ctx || !camera) return fail(ctx, RT_ERR_INVALID_ARG, "rt_set_camera: NULL argument");
+    ctx->cam = *camera;
+    return RT_OK;
+}
+
+int rt_get_camera(const rt_ctx* ctx, rt_camera* camera) {
+    if (!ctx || !camera) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_get_camera: NULL argument");
+    *camera = ctx->cam;
+    return RT_OK;
+}
+
+// CameraForwardDirection / CameraRightDirection / CameraUpDirection (RayTracer.cs:511-523):
+// double trig of the float yaw/pitch, each component cast to float; Up = Cross(Right, Fwd).
+// View params (Tick, :892-896): planeHeight = 0.3f * (float)Math.Tan(30f * (MathF.PI/180f)) * 2,
+// planeWidth = planeHeight * ((float)width / height).
+int rt_camera_view(const rt_camera* c, int width, int height, rt_view* out) {
+    if (!c || !out || width <= 0 || height <= 0) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_camera_view: bad args");
+    const double p = (double)c->pitch, y = (double)c->yaw;
+    const H3 f{(float)(std::cos(p) * std::sin(y)), (float)-std::sin(p), (float)(std::cos(p) * std::cos(y))};
+    const H3 r{(float)std::cos(y), 0.0f, (float)-std::sin(y)};
+    const H3 u = hcross(r, f);
+    out->position = c->position;
+    out->right = rt_vec3{r.x, r.y, r.z};
+    out->up = rt_vec3{u.x, u.y, u.z};
+    out->forward = rt_vec3{f.x, f.y, f.z};
+    const float near_clip = 0.3f, fov = 60.0f;
+    const float deg2rad = (float)M_PI / 180.0f;  // MathHelper.DegreesToRadians: d * (MathF.PI / 180f)
+    const float rad = (fov * 0.5f) * deg2rad;
+    const float plane_height = near_clip * (float)std::tan((double)rad) * 2;
+    const float aspect = (float)width / (float)height;
+    out->plane_width = plane_height * aspect;
+    out->plane_height = plane_height;
+    out->near_clip = near_clip;
+    return RT_OK;
+}
+
+// OnKeyPress, RayTracer.cs:543-554: position +/- direction * (0.05, 0.05, 0.05).
+int rt_camera_on_key(rt_camera* c, int key) {
+    if (!c) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_camera_on_key: NULL camera");
+    rt_view v;
+    rt_camera_view(c, 1, 1, &v);
+    const float m = 0.05f;
+    rt_vec3 dir;
+    float sign;
+    switch (key) {
+        case RT_KEY_W: dir = v.forward, sign = 1.0f; break;
+        case RT_KEY_A: dir = v.right, sign = -1.0f; break;
+        case RT_KEY_S: dir = v.forward, sign = -1.0f; break;
+        case RT_KEY_D: dir = v.right, sign = 1.0f; break;
+        case RT_KEY_SPACE: dir = v.up, sign = -1.0f; break;
+        case RT_KEY_SHIFT: dir = v.up, sign = 1.0f; break;
+        default: return RT_OK;  // `_ => _cameraPosition`
+    }
+    const rt_vec3 d{dir.x * m, dir.y * m, dir.z * m};
+    if (sign > 0) c->position = rt_vec3{c->position.x + d.x, c->position.y + d.y, c->position.z + d.z};
+    else c->position = rt_vec3{c->position.x - d.x, c->position.y - d.y, c->position.z - d.z};
+    return RT_OK;
+}
+
+// OnMouseMove, RayTracer.cs:1058-1061: _yaw += DeltaX / 360; _pitch += DeltaY / 360.
+int rt_camera_on_mouse_move(rt_camera* c, float dx, float dy) {
+    if (!c) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_camera_on_mouse_move: NULL camera");
+    c->yaw = c->yaw + dx / 360.0f;
+    c->pitch = c->pitch + dy / 360.0f;
+    return RT_OK;
+}
+
+int rt_render_device(rt_ctx* ctx, int width, int height, int32_t* d_pixels, void* hip_stream) {
+    int rc = check_ctx(ctx, width, height);
+    if (rc != RT_OK) return rc;
+    if (!d_pixels) return fail(ctx, RT_ERR_INVALID_ARG, "NULL d_pixels");
+    if (ctx->n_gpus != 1) return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_device needs a single-GPU context");
+    Device& d = ctx->dev[0];
+    DeviceGuard guard(d.id);
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : d.stream;
+    rc = trace_bands(ctx, d, s, width, height, height, 0, 1, d_pixels, nullptr);
+    if (rc == RT_OK) {
+        ctx->frames++;
+        ctx->pixels += (uint64_t)width * (uint64_t)height;
+    }
+    return rc;
+}
+
+int rt_render_bands(rt_ctx* ctx, int width, int height, int band_rows, int band_first, int band_step,
+                    int32_t* d_out, void* hip_stream, int* out_n_bands) {
+    int rc = check_ctx(ctx, width, height);
+    if (rc != RT_OK) return rc;
+    if (band_rows <= 0 || band_first < 0 || band_step <= 0 || !d_out)
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_bands: bad band arguments");
+    if (ctx->n_gpus != 1) return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_bands needs a single-GPU context");
+    Device& d = ctx->dev[0];
+    DeviceGuard guard(d.id);
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : d.stream;
+    int nb = 0;
+    rc = trace_bands(ctx, d, s, width, height, band_rows, band_first, band_step, d_out, &nb);
+    if (out_n_bands) *out_n_bands = nb;
+    if (rc == RT_OK) ctx->pixels += (uint64_t)nb * band_rows * width;
+    return rc;
+}
+
+int rt_scatter_bands(rt_ctx* ctx, int width, int height, int band_rows, int band_first, int band_step,
+                     const int32_t* d_bands, int32_t* d_frame, void* hip_stream) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "NULL context");
+    if (width <= 0 || height <= 0 || band_rows <= 0 || band_first < 0 || band_step <= 0 || !d_bands || !d_frame)
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_scatter_bands: bad arguments");
+    Device& d = ctx->dev[0];
+    DeviceGuard guard(d.id);
+    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : d.stream;
+    const int nb = bands_of(height, band_rows, band_first, band_step);
+    int e = launch_scatter_bands(d_bands, d_frame, width, height, band_rows, band_first, band_step, nb, s);
+    if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "scatter launch: %s", hipGetErrorString((hipError_t)e));
+    return RT_OK;
+}
+
+int rt_register_host(rt_ctx* ctx, void* host_ptr, size_t bytes) {
+    if (!ctx || !host_ptr || !bytes) return fail(ctx, RT_ERR_INVALID_ARG, "rt_register_host: bad arguments");
+    DeviceGuard guard(ctx->dev[0].id);
+    HIP_TRY(ctx, hipHostRegister(host_ptr, bytes, hipHostRegisterDefault));
+    return RT_OK;
+}
+
+int rt_unregister_host(rt_ctx* ctx, void* host_ptr) {
+    if (!ctx || !host_ptr) return fail(ctx, RT_ERR_INVALID_ARG, "rt_unregister_host: bad arguments");
+    DeviceGuard guard(ctx->dev[0].id);
+    HIP_TRY(ctx, hipHostUnregister(host_ptr));
+    return RT_OK;
+}
+
+// Tick(): full frame into the caller's Surface.pixels, synchronous.
+int rt_render(rt_ctx* ctx, int width, int height, int32_t* pixels) {
+    int rc = check_ctx(ctx, width, height);
+    if (rc != RT_OK) return rc;
+    if (!pixels) return fail(ctx, RT_ERR_INVALID_ARG, "NULL pixels");
+    const size_t frame_bytes = (size_t)width * height * sizeof(int32_t);
+    Device& d0 = ctx->dev[0];
+    if (ctx->n_gpus == 1) {
+        DeviceGuard guard(d0.id);
+        rc = grow(ctx, (void**)&d0.d_frame, &d0.frame_cap, frame_bytes);
+        if (rc != RT_OK) return rc;
+        rc = trace_bands(ctx, d0, d0.stream, width, height, height, 0, 1, d0.d_frame, nullptr);
+        if (rc != RT_OK) return rc;
+    } else {
+        // interleaved row bands: band b -> device b % n; each device traces its
+        // band set into a padded slot; RCCL gathers the slots to device 0 over xGMI, where
+        // they are scattered back into the row-major frame.
+        const int n = ctx->n_gpus;
+        const int band_rows = 8;
+        const int max_nb = bands_of(height, band_rows, 0, n);
+        const size_t slot = (size_t)max_nb * band_rows * width;  // int32 elements per device
+        for (int g = 0; g < n; ++g) {
+            Device& d = ctx->dev[(size_t)g];
+            DeviceGuard guard(d.id);
+            rc = grow(ctx, (void**)&d.d_bands, &d.bands_cap, slot * sizeof(int32_t));
+            if (rc != RT_OK) return rc;
+            if (g == 0) {
+                rc = grow(ctx, (void**)&d.d_gather, &d.gather_cap, slot * n * sizeof(int32_t));
+                if (rc == RT_OK) rc = grow(ctx, (void**)&d.d_frame, &d.frame_cap, frame_bytes);
+                if (rc != RT_OK) return rc;
+            }
+            rc = trace_bands(ctx, d, d.stream, width, height, band_rows, g, n, d.d_bands, nullptr);
+            if (rc != RT_OK) return rc;
+        }
+        for (int g = 0; g < n; ++g) {
+            DeviceGuard guard(ctx->dev[(size_t)g].id);
+            begin_timed(ctx, ctx->dev[(size_t)g], 2);
+        }
+        if (g_rccl.GroupStart() != 0) return fail(ctx, RT_ERR_RCCL, "ncclGroupStart failed");
+        for (int g = 0; g < n; ++g) {
+            Device& d = ctx->dev[(size_t)g];
+            DeviceGuard guard(d.id);
+            ncclResult_t r = g_rccl.Gather(d.d_bands, g == 0 ? d.d_gather : nullptr, slot, ncclInt32, 0, d.comm,
+                                           d.stream);
+            if (r != 0) {
+                (void)g_rccl.GroupEnd();
+                return fail(ctx, RT_ERR_RCCL, "ncclGather: %s", g_rccl.GetErrorString ? g_rccl.GetErrorString(r) : "?");
+            }
+        }
+        if (g_rccl.GroupEnd() != 0) return fail(ctx, RT_ERR_RCCL, "ncclGroupEnd failed");
+        for (int g = 0; g < n; ++g) {
+            DeviceGuard guard(ctx->dev[(size_t)g].id);
+            end_timed(ctx->dev[(size_t)g]);
+        }
+        DeviceGuard guard(d0.id);
+        for (int g = 0; g < n; ++g) {
+            const int nb = bands_of(height, band_rows, g, n);
+            int e = launch_scatter_bands(d0.d_gather + slot * g, d0.d_frame, width, height, band_rows, g, n, nb,
+                                         d0.stream);
+            if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "scatter: %s", hipGetErrorString((hipError_t)e));
+        }
+    }
+    DeviceGuard guard(d0.id);
+    begin_timed(ctx, d0, 1);
+    HIP_TRY(ctx, hipMemcpyAsync(pixels, d0.d_frame, frame_bytes, hipMemcpyDeviceToHost, d0.stream));
+    end_timed(d0);
+    HIP_TRY(ctx, hipStreamSynchronize(d0.stream));
+    ctx->frames++;
+    ctx->pixels += (uint64_t)width * (uint64_t)height;
+    return RT_OK;
+}
+
+int rt_get_stats(rt_ctx* ctx, rt_stats* out) {
+    if (!ctx || !out) return fail(ctx, RT_ERR_INVALID_ARG, "rt_get_stats: NULL argument");
+    std::memset(out, 0, sizeof *out);
+    unsigned long long c[4] = {0, 0, 0, 0};
+    for (Device& d : ctx->dev) {
+        DeviceGuard guard(d.id);
+        HIP_TRY(ctx, hipDeviceSynchronize());
+        drain_events(ctx, d);
+        unsigned long long h[4];
+        HIP_TRY(ctx, hipMemcpy(h, d.d_counters, sizeof h, hipMemcpyDeviceToHost));
+        for (int i = 0; i < 4; ++i) c[i] += h[i];
+    }
+    out->frames = ctx->frames;
+    out->pixels = ctx->pixels;
+    out->primary_rays = c[0];
+    out->reflect_rays = c[1];
+    out->shadow_rays = c[2];
+    const uint64_t S = (uint64_t)ctx->layout.S, P = (uint64_t)ctx->layout.P;
+    out->sphere_tests = (c[0] + c[1] + c[2]) * S;
+    out->plane_tests = (c[0] + c[1]) * P;
+    out->launches = ctx->launches;
+    out->kernel_ms = ctx->kernel_ms;
+    out->last_kernel_ms = ctx->last_kernel_ms;
+    out->copy_ms = ctx->copy_ms;
+    out->gather_ms = ctx->gather_ms;
+    return RT_OK;
+}
+
+int rt_reset_stats(rt_ctx* ctx) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "NULL context");
+    for (Device& d : ctx->dev) {
+        DeviceGuard guard(d.id);
+        HIP_TRY(ctx, hipDeviceSynchronize());
+        drain_events(ctx, d);
+        HIP_TRY(ctx, hipMemset(d.d_counters, 0, 4 * sizeof(unsigned long long)));
+    }
+    ctx->frames = ctx->pixels = ctx->launches = 0;
+    ctx->kernel_ms = ctx->last_kernel_ms = ctx->copy_ms = ctx->gather_ms = 0;
+    return RT_OK;
+}
+
+}  // extern "C"

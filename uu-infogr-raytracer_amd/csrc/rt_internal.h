@@ -1,0 +1,76 @@
+// rt_internal.h -- device-side scene layout and launch interface shared by the HIP
+// kernels (rt_kernel.hip) and the C-ABI host code (rt_api.cpp).
+//
+// Scene layout in HBM (one contiguous, 16-byte aligned allocation per context/device,
+// read through the scalar cache: every loop over primitives is wave-uniform):
+//   DevSphere  [S]   {center.xyz, radius^2}                 16 B   intersection loops
+//   DevMaterial[S+P] sphere materials then plane materials  64 B   shading (per-lane gather)
+//   DevPlane   [P]   {center, c.n, normal, e1, e2}          64 B
+//   DevLight   [L]   {position, intensity, |p|^2 terms}     32 B
+// Everything that the reference recomputes per call but that depends only on scene
+// constants (radius^2 :336, dot(center,normal) :594, checkerboard basis e1/e2 :760-765,
+// ambient*Ka :778/:873, dot(light,light) for the shadow ray :617) is computed once on the
+// host with the same binary32 operations, which yields bit-identical values.
+#pragma once
+#include <stdint.h>
+
+namespace rtk {
+
+struct DevSphere {
+    float cx, cy, cz, r2;
+};
+
+enum : uint32_t { MAT_MIRROR = 1u, MAT_DIFFUSE = 2u, MAT_SPEC = 4u };
+
+enum : uint32_t { POW_GENERIC = 0u, POW_ONE = 1u, POW_HALF = 2u, POW_TWO = 3u };
+
+struct DevMaterial {
+    float kd[3];
+    float amb[3];   // ambient * Ka  (RayTracer.cs:778, :873)
+    float ks[3];
+    float n;
+    float km[3];
+    uint32_t flags;  // MAT_* (RayTracer.cs:85-93)
+    uint32_t pow_kind;  // POW_* fast paths for Math.Pow(x, n) (exact; see rt_kernel.hip)
+    uint32_t pad;
+};
+
+struct DevPlane {
+    float cx, cy, cz, cn;  // center, dot(center, normal)
+    float nx, ny, nz, pad0;
+    float e1x, e1y, e1z, pad1;
+    float e2x, e2y, e2z, pad2;
+};
+
+struct DevLight {
+    float px, py, pz, intensity;
+    float a;      // dot(p, p)       : IntersectsSphere's `a` for a shadow ray (dir = position)
+    float a2;     // 2 * a
+    float a4;     // 4 * a
+    float pad;
+};
+
+// Per-launch parameters (passed by value as the kernel argument block).
+struct LaunchParams {
+    const DevSphere* sph;
+    const DevMaterial* mat;  // [S + P]
+    const DevPlane* pl;
+    const DevLight* li;
+    int S, P, L, limit;
+    // view, RayTracer.cs:511-523 and :892-896 (computed on the host)
+    float cam[3], right[3], up[3], fwd[3];
+    float pw, ph, nearc;
+    int W, H;
+    // row mapping: local row r -> band (band_first + (r / band_rows) * band_step),
+    // global row = band * band_rows + r % band_rows; pixel written at out[r * W + x].
+    int band_rows, band_first, band_step, local_rows;
+    int32_t* out;
+    unsigned long long* counters;  // [0] primary, [1] reflect, [2] shadow
+};
+
+// Launchers (rt_kernel.hip).  Return hipError_t as int.
+int launch_trace(const LaunchParams& p, void* stream);
+int launch_scatter_bands(const int32_t* bands, int32_t* frame, int W, int H, int band_rows, int band_first,
+                         int band_step, int n_bands, void* stream);
+
+}  // namespace rtk

@@ -1,0 +1,388 @@
+// rt_kernel.hip -- gfx950 kernels for the per-pixel Whitted trace of
+// Raytracer/RayTracer.cs (TracePixel :962-1002 -> TraceSphere/TracePlane :729-876 ->
+// IntersectsSphere/IntersectPlane :590-642 -> IntersectShadowLight :573-582 ->
+// *PhongShading :652-708 -> TraceSecondaryRay :789-826 -> ShiftColor :1046-1052).
+//
+// Design (MI355X-first, not a translation of the C# recursion):
+//  * one wave64 lane per pixel; a wave covers an 8x8 pixel tile, a 256-thread workgroup
+//    a 16x16 tile (ray coherence -> fewer divergent primitive hits per wave);
+//  * the scene is tiny (< 6 KB at 64 spheres) and every loop over spheres / planes / lights
+//    is wave-uniform, so primitive data is read with scalar loads (SGPR operands);
+//  * the reference shades EVERY hit primitive and recurses from each mirror hit; only the
+//    nearest (by the reference's own selection rules) reaches the pixel, so each lane walks
+//    a single chain of segments forward (intersection only), pushing one record per
+//    shaded mirror level onto a per-lane stack, then folds colours backward in the
+//    reference's exact order: mirror term, then each light in order, then ambient
+//    (RayTracer.cs:739-778, :850-873).  Bit-identical to the all-hit recursion.
+//  * arithmetic is IEEE binary32 with no FMA contraction (-ffp-contract=off), correctly
+//    rounded '/' and sqrt, IEEE-754-2019 maximum/minimum for .NET Math.Max/Min, f64 where
+//    the reference uses Math.Pow, and .NET's (int) conversion (NaN/overflow -> INT_MIN).
+#include <hip/hip_runtime.h>
+
+#include "rt_internal.h"
+
+namespace rtk {
+
+struct f3 {
+    float x, y, z;
+};
+
+__device__ __forceinline__ f3 mk(float x, float y, float z) { return f3{x, y, z}; }
+__device__ __forceinline__ f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+__device__ __forceinline__ f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+__device__ __forceinline__ f3 mul(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+__device__ __forceinline__ f3 scale(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+// Vector3.Dot: (x*x') + (y*y') + (z*z')
+__device__ __forceinline__ float dot(f3 a, f3 b) { return ((a.x * b.x) + (a.y * b.y)) + (a.z * b.z); }
+// Vector3.Normalize: s = 1f / MathF.Sqrt(x*x + y*y + z*z); v * s
+__device__ __forceinline__ f3 normalize(f3 a) {
+    float s = 1.0f / __builtin_sqrtf(dot(a, a));
+    return scale(a, s);
+}
+// Math.Max(x, 0f) / Math.Min(a, b) on .NET Core 3.0+: IEEE 754-2019 maximum / minimum
+// (NaN propagates, -0 < +0) -> v_maximum3_f32 / v_minimum3_f32 on gfx950.
+__device__ __forceinline__ float nmax0(float a) { return __builtin_elementwise_maximum(a, 0.0f); }
+__device__ __forceinline__ float nmin(float a, float b) { return __builtin_elementwise_minimum(a, b); }
+
+// (int)float on .NET 6 x64 (cvttss2si): NaN or out of range -> int.MinValue.
+__device__ __forceinline__ int32_t net_f2i(float v) {
+    return (v >= -2147483648.0f && v < 2147483648.0f) ? (int32_t)v : (int32_t)0x80000000;
+}
+
+// (float)Math.Pow((double)x, (double)n) for the shading exponent.  Exact fast paths:
+// n == 1 -> x; n == 2 -> x*x (the double product of two floats is exact, so one float
+// rounding of it equals binary32 x*x); n == 0.5 -> binary32 sqrt (a double result within
+// glibc pow's 0.54 ulp can never straddle a binary32 rounding boundary of sqrt(float):
+// the exact root is >= 2^-49 relative away from every binary32 midpoint).  Other
+// exponents use the device's f64 pow.
+__device__ __forceinline__ float spec_pow(float x, const DevMaterial& m) {
+    switch (m.pow_kind) {
+        case POW_ONE: return x;
+        case POW_HALF: return __builtin_sqrtf(x);
+        case POW_TWO: return x * x;
+        default: return (float)pow((double)x, (double)m.n);
+    }
+}
+
+// IntersectsSphere, RayTracer.cs:613-642, epsilon 0, for nearest-hit selection.  Returns
+// min(max(t1,0), max(t2,0)) when the discriminant is >= 0, else 0; callers select only
+// t > 0 (primary) / t - 0.01 > 0 (secondary), which is exactly the reference's
+// collision-or-0 distance under either rule.  a4 = 4*a and a2 = 2*a are per-ray.
+__device__ __forceinline__ float sphere_t(f3 o, f3 d, float a2, float a4, const DevSphere& s) {
+    f3 oc = sub(o, mk(s.cx, s.cy, s.cz));
+    float b = 2.0f * dot(oc, d);
+    float c = dot(oc, oc) - s.r2;
+    float disc = b * b - a4 * c;
+    float t = 0.0f;
+    if (disc >= 0.0f) {
+        float sq = __builtin_sqrtf(disc);  // == (float)Math.Sqrt((double)disc)
+        float t2 = (-b + sq) / a2;
+        float t1 = (-b - sq) / a2;
+        t = nmin(nmax0(t1), nmax0(t2));
+    }
+    return t;
+}
+
+// IntersectsSphere with epsilon 0.001 for the shadow ray of IntersectShadowLight
+// (origin = hit point, direction = light POSITION, RayTracer.cs:574-578).
+__device__ __forceinline__ bool shadow_blocked(f3 hp, const DevLight& l, const DevSphere& s) {
+    f3 oc = sub(hp, mk(s.cx, s.cy, s.cz));
+    f3 lp = mk(l.px, l.py, l.pz);
+    float b = 2.0f * dot(oc, lp);
+    float c = dot(oc, oc) - s.r2;
+    float disc = b * b - l.a4 * c;
+    if (disc >= 0.0f) {
+        float sq = __builtin_sqrtf(disc);
+        float t2 = (-b + sq) / l.a2;
+        float t1 = (-b - sq) / l.a2;
+        float te = nmin(nmax0(t1 - 0.001f), nmax0(t2 - 0.001f));
+        return te > 0.0f;
+    }
+    return false;
+}
+
+// IntersectPlane, RayTracer.cs:590-604: t = (((-o.x*n.x) - o.y*n.y) - o.z*n.z + c.n) / d.n
+__device__ __forceinline__ float plane_t(f3 o, f3 d, const DevPlane& p) {
+    float num = ((-o.x * p.nx - o.y * p.ny) - o.z * p.nz) + p.cn;
+    return num / dot(d, mk(p.nx, p.ny, p.nz));
+}
+
+// Shading of one shaded hit (TraceSphere :847-873 / TracePlane :736-778): the colour is
+// accumulated in the reference's order -- mirror term (from the deeper segment `sec`),
+// then each light, then ambient.  Returns the colour; adds shadow rays to *n_shadow.
+__device__ __forceinline__ f3 shade(const LaunchParams& p, bool is_sphere, int prim, f3 hp, f3 d, float t, f3 sec,
+                                 unsigned* n_shadow) {
+    const DevMaterial& m = p.mat[is_sphere ? prim : p.S + prim];
+    const uint32_t flags = m.flags;
+    f3 normal;
+    float tile = 1.0f;
+    if (is_sphere) {
+        const DevSphere& s = p.sph[prim];
+        normal = normalize(sub(hp, mk(s.cx, s.cy, s.cz)));  // SpherePhongShading :706
+    } else {
+        const DevPlane& pl = p.pl[prim];
+        normal = mk(pl.nx, pl.ny, pl.nz);
+        // checkerboard, :766-770: ((int)u + (int)v) & 1, unchecked int add
+        float u = dot(mk(pl.e1x, pl.e1y, pl.e1z), hp);
+        float v = dot(mk(pl.e2x, pl.e2y, pl.e2z), hp);
+        tile = (float)(int32_t)(((uint32_t)net_f2i(u) + (uint32_t)net_f2i(v)) & 1u);
+    }
+    f3 col = mk(0.0f, 0.0f, 0.0f);
+    if (flags & MAT_MIRROR) col = add(col, mul(sec, mk(m.km[0], m.km[1], m.km[2])));
+    if (flags & MAT_DIFFUSE) {
+        const f3 view = normalize(d);  // ShapePhongShading :668 (not negated)
+        // sphere: (1 / t) * t (:866);  plane: (float)(1 / Math.Pow(t, 2)) (:754), exact as 1/(t*t) in f64
+        const float att = is_sphere ? (1.0f / t) * t : (float)(1.0 / ((double)t * (double)t));
+        const f3 kd = mk(m.kd[0], m.kd[1], m.kd[2]);
+        for (int li = 0; li < p.L; ++li) {
+            const DevLight& l = p.li[li];
+            bool blocked = false;
+            for (int i = 0; i < p.S && !blocked; ++i) blocked = shadow_blocked(hp, l, p.sph[i]);
+            const float inten = blocked ? 0.0f : l.intensity;
+            // ShapePhongShading, :665-695
+            const f3 ldir = normalize(sub(mk(l.px, l.py, l.pz), hp));
+            f3 ph = scale(kd, nmax0(dot(normal, ldir)));
+            f3 spec = mk(0.0f, 0.0f, 0.0f);
+            if (flags & MAT_SPEC) {
+                f3 rs = sub(ldir, scale(normal, 2.0f * dot(ldir, normal)));
+                float sp = spec_pow(nmax0(dot(view, normalize(rs))), m);
+                spec = mul(mk(m.ks[0], m.ks[1], m.ks[2]), mk(sp, sp, sp));
+            }
+            ph = add(ph, spec);
+            const float ia = inten * att;
+            f3 term = mul(mk(ia, ia, ia), ph);
+            if (!is_sphere) {
+                term = mul(term, mk(tile, tile, tile));
+                term = mk(nmax0(term.x), nmax0(term.y), nmax0(term.z));  // .Max(0f), :775
+            }
+            col = add(col, term);
+        }
+        *n_shadow += (unsigned)p.L;
+    }
+    return add(col, mk(m.amb[0], m.amb[1], m.amb[2]));
+}
+
+// ShiftColor, :1046-1052: Math.Clamp (NaN passes), * 255f, Math.Floor, (int), (byte).
+__device__ __forceinline__ uint32_t shift_channel(float c) {
+    if (!(c == c)) return 0u;  // NaN -> (int) int.MinValue -> (byte) 0
+    float cl = c < 0.0f ? 0.0f : (c > 1.0f ? 1.0f : c);
+    return (uint32_t)(int32_t)__builtin_floorf(cl * 255.0f) & 255u;
+}
+
+// Per-lane level stack.  Records: a = {hit point, t}, b = {incoming direction, primitive code}.
+template <int K, bool SCRATCH>
+struct LevelStack;
+
+// Register stack: K fixed, static indices only (shift on push/pop) so it stays in VGPRs.
+template <int K>
+struct LevelStack<K, false> {
+    float4 a[K], b[K];
+    int n = 0;
+    __device__ __forceinline__ void push(float4 x, float4 y) {
+#pragma unroll
+        for (int i = K - 1; i > 0; --i) {
+            a[i] = a[i - 1];
+            b[i] = b[i - 1];
+        }
+        a[0] = x;
+        b[0] = y;
+        ++n;
+    }
+    __device__ __forceinline__ void pop(float4& x, float4& y) {
+        x = a[0];
+        y = b[0];
+#pragma unroll
+        for (int i = 0; i < K - 1; ++i) {
+            a[i] = a[i + 1];
+            b[i] = b[i + 1];
+        }
+        --n;
+    }
+};
+
+// Deep-recursion stack (recursion limits >= 8): dynamically indexed, lives in scratch.
+template <int K>
+struct LevelStack<K, true> {
+    float4 a[K], b[K];
+    int n = 0;
+    __device__ __forceinline__ void push(float4 x, float4 y) {
+        a[n] = x;
+        b[n] = y;
+        ++n;
+    }
+    __device__ __forceinline__ void pop(float4& x, float4& y) {
+        --n;
+        x = a[n];
+        y = b[n];
+    }
+};
+
+__device__ __forceinline__ unsigned wave_sum(unsigned v) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+template <int K, bool SCRATCH>
+__global__ __launch_bounds__(256) void trace_kernel(LaunchParams p) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int r = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const int band = p.band_first + (r / p.band_rows) * p.band_step;
+    const int y = band * p.band_rows + (r % p.band_rows);
+    const bool valid = x < p.W && r < p.local_rows && y < p.H;
+
+    unsigned n_prim = 0, n_refl = 0, n_shadow = 0;
+    if (valid) {
+        n_prim = 1;
+        const f3 cam = mk(p.cam[0], p.cam[1], p.cam[2]);
+        // TracePixel primary ray, :963-971 (no half-pixel offset)
+        const float px = (float)x / (float)p.W - 0.5f;
+        const float py = (float)y / (float)p.H - 0.5f;
+        const float lx = px * p.pw, ly = py * p.ph, lz = 1.0f * p.nearc;
+        f3 vp = add(add(add(cam, scale(mk(p.right[0], p.right[1], p.right[2]), lx)),
+                        scale(mk(p.up[0], p.up[1], p.up[2]), ly)),
+                    scale(mk(p.fwd[0], p.fwd[1], p.fwd[2]), lz));
+        f3 d = normalize(sub(vp, cam));
+        f3 o = cam;
+
+        LevelStack<K, SCRATCH> stk;
+        f3 leaf = mk(0.0f, 0.0f, 0.0f);
+        int count = 0;
+        for (;;) {
+            const bool primary = count == 0;
+            const float a = dot(d, d);
+            const float a2 = 2.0f * a, a4 = 4.0f * a;
+            // nearest sphere: TracePixel rule (:977) for the primary ray, the asymmetric
+            // TraceSecondaryRay rule (:804-806) for reflected rays
+            float best_s = __builtin_inff();
+            int win_s = -1;
+            for (int i = 0; i < p.S; ++i) {
+                const float t = sphere_t(o, d, a2, a4, p.sph[i]);
+                const float tm = t - 0.01f;
+                const bool sel = primary ? (t > 0.0f && best_s > t) : (tm > 0.0f && tm < best_s);
+                if (sel) {
+                    best_s = t;
+                    win_s = i;
+                }
+            }
+            // nearest plane (:987, :819)
+            float best_p = __builtin_inff();
+            int win_p = -1;
+            for (int i = 0; i < p.P; ++i) {
+                const float t = plane_t(o, d, p.pl[i]);
+                if (t > 0.0f && t < best_p) {
+                    best_p = t;
+                    win_p = i;
+                }
+            }
+            bool is_sphere;
+            float t;
+            int prim;
+            if (best_s < best_p) {  // :993 / :825
+                is_sphere = true;
+                t = best_s;
+                prim = win_s;
+            } else if (win_p >= 0) {
+                is_sphere = false;
+                t = best_p;
+                prim = win_p;
+            } else {
+                break;  // nothing hit: plane colour stays Zero
+            }
+            if (t - 0.01f <= 0.0f) break;  // too close: Zero (:731, :839)
+            if (count > p.limit) {        // terminal segment: Zero / One (:734, :843)
+                if (!is_sphere) leaf = mk(1.0f, 1.0f, 1.0f);
+                break;
+            }
+            // shaded hit: record it; mirror hits continue with the reflected segment
+            const f3 hp = add(o, scale(d, t));
+            const int code = is_sphere ? prim : ~prim;
+            stk.push(make_float4(hp.x, hp.y, hp.z, t), make_float4(d.x, d.y, d.z, __int_as_float(code)));
+            const uint32_t flags = p.mat[is_sphere ? prim : p.S + prim].flags;
+            if (!(flags & MAT_MIRROR)) break;
+            f3 normal;
+            if (is_sphere) {
+                const DevSphere& s = p.sph[prim];
+                normal = normalize(sub(hp, mk(s.cx, s.cy, s.cz)));  // :854
+            } else {
+                const DevPlane& pl = p.pl[prim];
+                normal = mk(pl.nx, pl.ny, pl.nz);
+            }
+            d = sub(d, scale(normal, 2.0f * dot(d, normal)));  // CalculateReflectionRay :718-720
+            o = hp;
+            ++count;
+            ++n_refl;
+        }
+        // backward fold: every recorded hit is shaded in reverse order; a mirror hit
+        // consumes the colour of the segment after it (levels 0..limit push at most one
+        // record each, so K = limit + 1 records suffice)
+        f3 col = leaf;
+        while (stk.n > 0) {
+            float4 ra, rb;
+            stk.pop(ra, rb);
+            const int code = __float_as_int(rb.w);
+            const bool is_s = code >= 0;
+            col = shade(p, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z), ra.w, col,
+                        &n_shadow);
+        }
+        const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
+        p.out[(size_t)r * (size_t)p.W + (size_t)x] = (int32_t)px32;
+    }
+
+    // work counters: one atomic per wave per counter
+    n_prim = wave_sum(n_prim);
+    n_refl = wave_sum(n_refl);
+    n_shadow = wave_sum(n_shadow);
+    if (lane == 0 && (n_prim | n_refl | n_shadow)) {
+        atomicAdd(&p.counters[0], (unsigned long long)n_prim);
+        atomicAdd(&p.counters[1], (unsigned long long)n_refl);
+        atomicAdd(&p.counters[2], (unsigned long long)n_shadow);
+    }
+}
+
+// Reassemble packed row bands (rt_render_bands layout) into a row-major frame.
+__global__ __launch_bounds__(256) void scatter_bands_kernel(const int32_t* __restrict__ bands,
+                                                            int32_t* __restrict__ frame, int W, int H, int band_rows,
+                                                            int band_first, int band_step, int local_rows) {
+    const size_t total = (size_t)local_rows * (size_t)W;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int r = (int)(i / (size_t)W);
+        const int x = (int)(i - (size_t)r * W);
+        const int y = (band_first + (r / band_rows) * band_step) * band_rows + r % band_rows;
+        if (y < H) frame[(size_t)y * W + x] = bands[i];
+    }
+}
+
+int launch_trace(const LaunchParams& p, void* stream) {
+    if (p.local_rows <= 0 || p.W <= 0) return (int)hipSuccess;
+    const dim3 grid((unsigned)((p.W + 15) / 16), (unsigned)((p.local_rows + 15) / 16));
+    const dim3 block(256);
+    hipStream_t s = (hipStream_t)stream;
+    const int need = p.limit + 1;  // levels 0..limit can push a mirror record
+    if (need <= 1)
+        hipLaunchKernelGGL((trace_kernel<1, false>), grid, block, 0, s, p);
+    else if (need <= 2)
+        hipLaunchKernelGGL((trace_kernel<2, false>), grid, block, 0, s, p);
+    else if (need <= 4)
+        hipLaunchKernelGGL((trace_kernel<4, false>), grid, block, 0, s, p);
+    else if (need <= 8)
+        hipLaunchKernelGGL((trace_kernel<8, false>), grid, block, 0, s, p);
+    else
+        hipLaunchKernelGGL((trace_kernel<64, true>), grid, block, 0, s, p);
+    return (int)hipGetLastError();
+}
+
+int launch_scatter_bands(const int32_t* bands, int32_t* frame, int W, int H, int band_rows, int band_first,
+                         int band_step, int n_bands, void* stream) {
+    const size_t total = (size_t)n_bands * band_rows * W;
+    if (total == 0) return (int)hipSuccess;
+    size_t blocks = (total + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    hipLaunchKernelGGL(scatter_bands_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, bands, frame,
+                       W, H, band_rows, band_first, band_step, n_bands * band_rows);
+    return (int)hipGetLastError();
+}
+
+}  // namespace rtk

@@ -1,0 +1,191 @@
+"""raytracer_hip -- host-side mirror of the reference's plugin surface over libraytracer_hip.
+
+Reference surface (Raytracer/RayTracer.cs, Raytracer/surface.cs):
+
+    Surface(w, h)                  surface.cs:15-20   width, height, int[] pixels, Clear(c)
+    RayTracer(Surface screen)      RayTracer.cs:535   .screen, Tick(), OnKeyPress(e), OnMouseMove(e)
+
+Here `Surface.pixels` is a numpy int32 array (0x00RRGGBB, row-major y*width+x), and
+`RayTracer.Tick()` renders the frame on the GPU through the C ABI (rt_render) straight into
+it.  There is no CPU fallback: constructing a RayTracer without the built library or
+without a gfx950 device raises RayTracerError.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import abi, scenes
+from .abi import RayTracerError, check, load_library
+
+__all__ = ["Surface", "RayTracer", "Context", "RayTracerError", "scenes", "abi", "load_library",
+           "device_count", "camera_view"]
+
+
+def device_count() -> int:
+    lib = load_library()
+    n = C.c_int(0)
+    check(lib, lib.rt_device_count(C.byref(n)))
+    return n.value
+
+
+def camera_view(camera: abi.rt_camera, width: int, height: int) -> abi.rt_view:
+    lib = load_library()
+    v = abi.rt_view()
+    check(lib, lib.rt_camera_view(C.byref(camera), width, height, C.byref(v)))
+    return v
+
+
+class Surface:
+    """surface.cs:7-46 -- the linear frame buffer the reference's Tick() fills."""
+
+    def __init__(self, w: int, h: int):
+        self.width = int(w)
+        self.height = int(h)
+        self.pixels = np.zeros(self.width * self.height, dtype=np.int32)
+
+    def Clear(self, c: int):  # surface.cs:43-46
+        self.pixels[:] = np.int32(c)
+
+    def image(self) -> np.ndarray:
+        return self.pixels.reshape(self.height, self.width)
+
+
+class Context:
+    """Thin owner of an rt_ctx*."""
+
+    def __init__(self, n_gpus: int = 1):
+        self.lib = load_library()
+        self.ptr = C.c_void_p()
+        check(self.lib, self.lib.rt_create(int(n_gpus), C.byref(self.ptr)))
+        self.n_gpus = n_gpus
+        self.scene = None
+
+    # -- lifetime ---------------------------------------------------------------
+    def close(self):
+        if self.ptr:
+            self.lib.rt_destroy(self.ptr)
+            self.ptr = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def _check(self, code):
+        return check(self.lib, code, self.ptr)
+
+    # -- scene / camera -----------------------------------------------------------
+    def set_scene(self, scene: scenes.Scene):
+        S, P, L = scene.c_arrays()
+        self._check(self.lib.rt_set_scene(self.ptr, S, len(scene.spheres), P, len(scene.planes), L,
+                                          len(scene.lights), abi.rt_vec3(*scene.ambient), scene.recursion_limit))
+        self._check(self.lib.rt_set_camera(self.ptr, C.byref(scene.c_camera())))
+        self.scene = scene
+
+    def set_camera(self, camera: abi.rt_camera):
+        self._check(self.lib.rt_set_camera(self.ptr, C.byref(camera)))
+
+    def get_camera(self) -> abi.rt_camera:
+        c = abi.rt_camera()
+        self._check(self.lib.rt_get_camera(self.ptr, C.byref(c)))
+        return c
+
+    # -- rendering ----------------------------------------------------------------
+    def render(self, width: int, height: int, out: np.ndarray | None = None) -> np.ndarray:
+        """Synchronous full frame into host memory (rt_render, the Tick() path)."""
+        if out is None:
+            out = np.empty(width * height, dtype=np.int32)
+        assert out.dtype == np.int32 and out.flags.c_contiguous and out.size == width * height
+        self._check(self.lib.rt_render(self.ptr, width, height, out.ctypes.data))
+        return out.reshape(height, width)
+
+    def render_device(self, width: int, height: int, d_ptr: int, stream: int = 0):
+        self._check(self.lib.rt_render_device(self.ptr, width, height, C.c_void_p(d_ptr), C.c_void_p(stream)))
+
+    def render_bands(self, width: int, height: int, band_rows: int, band_first: int, band_step: int, d_ptr: int,
+                     stream: int = 0) -> int:
+        nb = C.c_int(0)
+        self._check(self.lib.rt_render_bands(self.ptr, width, height, band_rows, band_first, band_step,
+                                             C.c_void_p(d_ptr), C.c_void_p(stream), C.byref(nb)))
+        return nb.value
+
+    def scatter_bands(self, width: int, height: int, band_rows: int, band_first: int, band_step: int,
+                      d_bands: int, d_frame: int, stream: int = 0):
+        self._check(self.lib.rt_scatter_bands(self.ptr, width, height, band_rows, band_first, band_step,
+                                              C.c_void_p(d_bands), C.c_void_p(d_frame), C.c_void_p(stream)))
+
+    def register_host(self, arr: np.ndarray):
+        self._check(self.lib.rt_register_host(self.ptr, C.c_void_p(arr.ctypes.data), arr.nbytes))
+
+    def unregister_host(self, arr: np.ndarray):
+        self._check(self.lib.rt_unregister_host(self.ptr, C.c_void_p(arr.ctypes.data)))
+
+    # -- stats ----------------------------------------------------------------------
+    def stats(self) -> dict:
+        s = abi.rt_stats()
+        self._check(self.lib.rt_get_stats(self.ptr, C.byref(s)))
+        return s.as_dict()
+
+    def reset_stats(self):
+        self._check(self.lib.rt_reset_stats(self.ptr))
+
+
+def bands_of(height: int, band_rows: int, first: int, step: int) -> int:
+    """Number of row bands b = first, first+step, ... with b*band_rows < height."""
+    total = (height + band_rows - 1) // band_rows
+    return (total - 1 - first) // step + 1 if first < total else 0
+
+
+class RayTracer:
+    """RayTracer.cs:437-1062, public surface only, rendering on MI355X.
+
+    `scene` defaults to the reference's hard-coded scene (RayTracer.cs:441-490).
+    """
+
+    _KEYS = {"W": abi.RT_KEY_W, "A": abi.RT_KEY_A, "S": abi.RT_KEY_S, "D": abi.RT_KEY_D,
+             "Space": abi.RT_KEY_SPACE, "LeftShift": abi.RT_KEY_SHIFT, "RightShift": abi.RT_KEY_SHIFT}
+
+    def __init__(self, screen: Surface, scene: scenes.Scene | None = None, n_gpus: int = 1):
+        self.screen = screen
+        self._ctx = Context(n_gpus)
+        sc = scene or scenes.reference(screen.width, screen.height)
+        self._ctx.set_scene(sc)
+        self._camera = sc.c_camera()
+        self._ctx.register_host(screen.pixels)  # pin Surface.pixels once (D2H lands in it)
+
+    def Tick(self):
+        """RayTracer.Tick(), RayTracer.cs:886-935: the whole frame, synchronously."""
+        self._ctx.set_camera(self._camera)
+        self._ctx.render(self.screen.width, self.screen.height, self.screen.pixels)
+
+    def OnKeyPress(self, key):
+        """RayTracer.OnKeyPress, RayTracer.cs:543-554 (key: 'W','A','S','D','Space','LeftShift'...)."""
+        code = self._KEYS.get(key, 0) if isinstance(key, str) else int(key)
+        check(self._ctx.lib, self._ctx.lib.rt_camera_on_key(C.byref(self._camera), code))
+
+    def OnMouseMove(self, delta_x: float, delta_y: float):
+        """RayTracer.OnMouseMove, RayTracer.cs:1058-1061."""
+        check(self._ctx.lib, self._ctx.lib.rt_camera_on_mouse_move(C.byref(self._camera), delta_x, delta_y))
+
+    @property
+    def camera(self) -> abi.rt_camera:
+        return self._camera
+
+    def stats(self) -> dict:
+        return self._ctx.stats()
+
+    def close(self):
+        if self._ctx.ptr:
+            try:
+                self._ctx.unregister_host(self.screen.pixels)
+            finally:
+                self._ctx.close()

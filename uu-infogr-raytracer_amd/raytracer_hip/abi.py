@@ -1,0 +1,134 @@
+"""ctypes mirror of include/raytracer_hip.h and the loader for libraytracer_hip.so.
+
+The shared library is the product: HIP kernels for gfx950 behind a plain C ABI.  There is
+no CPU fallback -- if the library is missing or no device is present, the calls below
+raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libraytracer_hip.so")
+
+RT_OK = 0
+RT_ERR_INVALID_ARG = -1
+RT_ERR_NO_DEVICE = -2
+RT_ERR_HIP = -3
+RT_ERR_NO_SCENE = -4
+RT_ERR_UNSUPPORTED = -5
+RT_ERR_RCCL = -6
+RT_ERR_OOM = -7
+RT_MAX_RECURSION_LIMIT = 63
+
+RT_KEY_W, RT_KEY_A, RT_KEY_S, RT_KEY_D, RT_KEY_SPACE, RT_KEY_SHIFT = 1, 2, 3, 4, 5, 6
+
+
+class rt_vec3(C.Structure):
+    _fields_ = [("x", C.c_float), ("y", C.c_float), ("z", C.c_float)]
+
+    def tuple(self):
+        return (self.x, self.y, self.z)
+
+
+class rt_material(C.Structure):
+    _fields_ = [("kd", rt_vec3), ("ka", rt_vec3), ("ks", rt_vec3), ("n", C.c_float), ("km", rt_vec3)]
+
+
+class rt_sphere(C.Structure):
+    _fields_ = [("center", rt_vec3), ("radius", C.c_float), ("material", rt_material)]
+
+
+class rt_plane(C.Structure):
+    _fields_ = [("center", rt_vec3), ("normal", rt_vec3), ("material", rt_material)]
+
+
+class rt_light(C.Structure):
+    _fields_ = [("position", rt_vec3), ("intensity", C.c_float)]
+
+
+class rt_camera(C.Structure):
+    _fields_ = [("position", rt_vec3), ("yaw", C.c_float), ("pitch", C.c_float)]
+
+
+class rt_view(C.Structure):
+    _fields_ = [
+        ("position", rt_vec3), ("right", rt_vec3), ("up", rt_vec3), ("forward", rt_vec3),
+        ("plane_width", C.c_float), ("plane_height", C.c_float), ("near_clip", C.c_float),
+    ]
+
+
+class rt_stats(C.Structure):
+    _fields_ = [
+        ("frames", C.c_uint64), ("pixels", C.c_uint64), ("primary_rays", C.c_uint64),
+        ("reflect_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("sphere_tests", C.c_uint64),
+        ("plane_tests", C.c_uint64), ("launches", C.c_uint64), ("kernel_ms", C.c_double),
+        ("last_kernel_ms", C.c_double), ("copy_ms", C.c_double), ("gather_ms", C.c_double),
+    ]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
+# (name, restype, argtypes) of every exported entry point declared in the header.
+EXPORTS = [
+    ("rt_abi_version", C.c_int, []),
+    ("rt_device_count", C.c_int, [C.POINTER(C.c_int)]),
+    ("rt_last_error", C.c_char_p, [C.c_void_p]),
+    ("rt_create", C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    ("rt_destroy", None, [C.c_void_p]),
+    ("rt_set_scene", C.c_int, [C.c_void_p, C.POINTER(rt_sphere), C.c_int, C.POINTER(rt_plane), C.c_int,
+                               C.POINTER(rt_light), C.c_int, rt_vec3, C.c_int]),
+    ("rt_set_camera", C.c_int, [C.c_void_p, C.POINTER(rt_camera)]),
+    ("rt_get_camera", C.c_int, [C.c_void_p, C.POINTER(rt_camera)]),
+    ("rt_camera_view", C.c_int, [C.POINTER(rt_camera), C.c_int, C.c_int, C.POINTER(rt_view)]),
+    ("rt_camera_on_key", C.c_int, [C.POINTER(rt_camera), C.c_int]),
+    ("rt_camera_on_mouse_move", C.c_int, [C.POINTER(rt_camera), C.c_float, C.c_float]),
+    ("rt_render", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    ("rt_register_host", C.c_int, [C.c_void_p, C.c_void_p, C.c_size_t]),
+    ("rt_unregister_host", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("rt_render_device", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p, C.c_void_p]),
+    ("rt_render_bands", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                  C.c_void_p, C.POINTER(C.c_int)]),
+    ("rt_scatter_bands", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                   C.c_void_p, C.c_void_p]),
+    ("rt_get_stats", C.c_int, [C.c_void_p, C.POINTER(rt_stats)]),
+    ("rt_reset_stats", C.c_int, [C.c_void_p]),
+]
+
+_lib = None
+
+
+class RayTracerError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"libraytracer_hip error {code}: {msg}")
+        self.code = code
+
+
+def load_library(path: str | None = None):
+    """Load libraytracer_hip.so (in-tree build).  Raises if it was not built."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise RuntimeError(
+            f"libraytracer_hip.so not found at {p}: run __graft_entry__.build() "
+            "(there is no CPU fallback)")
+    lib = C.CDLL(p, mode=C.RTLD_GLOBAL)
+    for name, res, args in EXPORTS:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def check(lib, code: int, ctx=None):
+    if code != RT_OK:
+        msg = lib.rt_last_error(ctx)
+        raise RayTracerError(code, msg.decode() if msg else "")
+    return code
