@@ -173,8 +173,8 @@ int rt_register_host(rt_ctx* ctx, void* host_ptr, size_t bytes);
 int rt_unregister_host(rt_ctx* ctx, void* host_ptr);
 
 /* Device-resident variant (single-GPU contexts): renders the frame into
- * d_pixels[width*height] on `hip_stream` (a hipStream_t, NULL = the context's own
- * stream) and returns without synchronising. */
+ * d_pixels[width*height] on `hip_stream` (a hipStream_t; NULL = the HIP null stream, as
+ * everywhere in HIP) and returns without synchronising. */
 int rt_render_device(rt_ctx* ctx, int width, int height, int32_t* d_pixels, void* hip_stream);
 
 /* Row-band shard (one process per GPU): renders the bands b = band_first,

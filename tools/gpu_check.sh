@@ -21,3 +21,9 @@ step() {
 step smoke 420 python -c "import __graft_entry__ as g; g.smoke()"
 step pytest_gpu 900 python -m pytest tests -m gpu -q -rf
 step bench 600 python bench.py "$@"
+if [ "${PROFILE:-0}" = "1" ]; then
+    export TMPDIR=/tmp
+    step profile 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
+        -- python3 bench.py --steps 100 --warmup 5 --no-cpu-baseline "$@"
+    find gpurun_out/prof -name "*kernel_stats.csv" -exec cat {} \;
+fi

@@ -322,8 +322,8 @@ int rt_create(int n_gpus, rt_ctx** out_ctx) {
             return rc;
         }
         hipError_t e = hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking);
-        if (e == hipSuccess) e = hipMalloc((void**)&d.d_counters, 4 * sizeof(unsigned long long));
-        if (e == hipSuccess) e = hipMemset(d.d_counters, 0, 4 * sizeof(unsigned long long));
+        if (e == hipSuccess) e = hipMalloc((void**)&d.d_counters, COUNTER_WORDS * sizeof(unsigned long long));
+        if (e == hipSuccess) e = hipMemset(d.d_counters, 0, COUNTER_WORDS * sizeof(unsigned long long));
         if (e != hipSuccess) {
             int rc = fail(ctx, RT_ERR_HIP, "device %d init: %s", d.id, hipGetErrorString(e));
             g_last_error = ctx->last_error;
@@ -516,7 +516,7 @@ int rt_render_device(rt_ctx* ctx, int width, int height, int32_t* d_pixels, void
     if (ctx->n_gpus != 1) return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_device needs a single-GPU context");
     Device& d = ctx->dev[0];
     DeviceGuard guard(d.id);
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : d.stream;
+    hipStream_t s = (hipStream_t)hip_stream;  // NULL = the HIP null stream
     rc = trace_bands(ctx, d, s, width, height, height, 0, 1, d_pixels, nullptr);
     if (rc == RT_OK) {
         ctx->frames++;
@@ -534,7 +534,7 @@ int rt_render_bands(rt_ctx* ctx, int width, int height, int band_rows, int band_
     if (ctx->n_gpus != 1) return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_bands needs a single-GPU context");
     Device& d = ctx->dev[0];
     DeviceGuard guard(d.id);
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : d.stream;
+    hipStream_t s = (hipStream_t)hip_stream;  // NULL = the HIP null stream
     int nb = 0;
     rc = trace_bands(ctx, d, s, width, height, band_rows, band_first, band_step, d_out, &nb);
     if (out_n_bands) *out_n_bands = nb;
@@ -549,7 +549,7 @@ int rt_scatter_bands(rt_ctx* ctx, int width, int height, int band_rows, int band
         return fail(ctx, RT_ERR_INVALID_ARG, "rt_scatter_bands: bad arguments");
     Device& d = ctx->dev[0];
     DeviceGuard guard(d.id);
-    hipStream_t s = hip_stream ? (hipStream_t)hip_stream : d.stream;
+    hipStream_t s = (hipStream_t)hip_stream;  // NULL = the HIP null stream
     const int nb = bands_of(height, band_rows, band_first, band_step);
     int e = launch_scatter_bands(d_bands, d_frame, width, height, band_rows, band_first, band_step, nb, s);
     if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "scatter launch: %s", hipGetErrorString((hipError_t)e));
@@ -650,9 +650,11 @@ int rt_get_stats(rt_ctx* ctx, rt_stats* out) {
         DeviceGuard guard(d.id);
         HIP_TRY(ctx, hipDeviceSynchronize());
         drain_events(ctx, d);
-        unsigned long long h[4];
-        HIP_TRY(ctx, hipMemcpy(h, d.d_counters, sizeof h, hipMemcpyDeviceToHost));
-        for (int i = 0; i < 4; ++i) c[i] += h[i];
+        std::vector<unsigned long long> h(COUNTER_WORDS);
+        HIP_TRY(ctx, hipMemcpy(h.data(), d.d_counters, COUNTER_WORDS * sizeof(unsigned long long),
+                               hipMemcpyDeviceToHost));
+        for (int slot = 0; slot < COUNTER_SLOTS; ++slot)
+            for (int i = 0; i < 4; ++i) c[i] += h[(size_t)slot * 4 + i];
     }
     out->frames = ctx->frames;
     out->pixels = ctx->pixels;
@@ -676,7 +678,7 @@ int rt_reset_stats(rt_ctx* ctx) {
         DeviceGuard guard(d.id);
         HIP_TRY(ctx, hipDeviceSynchronize());
         drain_events(ctx, d);
-        HIP_TRY(ctx, hipMemset(d.d_counters, 0, 4 * sizeof(unsigned long long)));
+        HIP_TRY(ctx, hipMemset(d.d_counters, 0, COUNTER_WORDS * sizeof(unsigned long long)));
     }
     ctx->frames = ctx->pixels = ctx->launches = 0;
     ctx->kernel_ms = ctx->last_kernel_ms = ctx->copy_ms = ctx->gather_ms = 0;

@@ -50,6 +50,11 @@ struct DevLight {
     float pad;
 };
 
+// Work counters: each workgroup adds its totals into slot (block id % COUNTER_SLOTS) so that
+// the atomics of thousands of workgroups do not serialise on one address.
+constexpr int COUNTER_SLOTS = 256;
+constexpr int COUNTER_WORDS = COUNTER_SLOTS * 4;
+
 // Per-launch parameters (passed by value as the kernel argument block).
 struct LaunchParams {
     const DevSphere* sph;
@@ -65,7 +70,7 @@ struct LaunchParams {
     // global row = band * band_rows + r % band_rows; pixel written at out[r * W + x].
     int band_rows, band_first, band_step, local_rows;
     int32_t* out;
-    unsigned long long* counters;  // [0] primary, [1] reflect, [2] shadow
+    unsigned long long* counters;  // COUNTER_SLOTS x {primary, reflect, shadow, pad}
 };
 
 // Launchers (rt_kernel.hip).  Return hipError_t as int.

@@ -331,14 +331,21 @@ __global__ __launch_bounds__(256) void trace_kernel(LaunchParams p) {
         p.out[(size_t)r * (size_t)p.W + (size_t)x] = (int32_t)px32;
     }
 
-    // work counters: one atomic per wave per counter
+    // work counters: wave sums -> LDS -> one workgroup total added to a spread slot
+    __shared__ unsigned red[4][3];
     n_prim = wave_sum(n_prim);
     n_refl = wave_sum(n_refl);
     n_shadow = wave_sum(n_shadow);
-    if (lane == 0 && (n_prim | n_refl | n_shadow)) {
-        atomicAdd(&p.counters[0], (unsigned long long)n_prim);
-        atomicAdd(&p.counters[1], (unsigned long long)n_refl);
-        atomicAdd(&p.counters[2], (unsigned long long)n_shadow);
+    if (lane == 0) {
+        red[wave][0] = n_prim;
+        red[wave][1] = n_refl;
+        red[wave][2] = n_shadow;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const unsigned v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+        const unsigned slot = (blockIdx.y * gridDim.x + blockIdx.x) % COUNTER_SLOTS;
+        if (v) atomicAdd(&p.counters[slot * 4 + threadIdx.x], (unsigned long long)v);
     }
 }
 
