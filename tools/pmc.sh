@@ -1,0 +1,24 @@
+#!/bin/bash
+# PMC passes on the trace kernel, one counter group per rocprofv3 run (gfx950 rules:
+# FETCH_SIZE and WRITE_SIZE in separate passes; never combined with tracing domains).
+# Usage (GPU box): bash tools/pmc.sh CONFIG [extra bench args]
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+CFG=${1:-C2}; shift || true
+OUT=gpurun_out/pmc_$CFG
+mkdir -p "$OUT"
+timeout -k 10 120 rocprofv3 -L > "$OUT/counters_list.txt" 2>&1 || true
+i=0
+for group in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE" \
+             "SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY" \
+             "SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INST_CYCLES_VMEM_RD TCP_TOTAL_CACHE_ACCESSES_sum" ; do
+    i=$((i+1))
+    echo "== pass $i: $group"
+    timeout -k 10 300 rocprofv3 --pmc $group --output-format csv -d "$OUT/p$i" -o run \
+        -- python3 bench.py --config "$CFG" --steps 20 --warmup 2 --no-cpu-baseline "$@" > "$OUT/p$i.log" 2>&1
+    rc=$?
+    echo "rc=$rc"
+    if [ $rc -ne 0 ] && grep -qiE "memory access fault|segmentation|core dumped" "$OUT/p$i.log"; then exit $rc; fi
+    if [ $rc -eq 124 ] || [ $rc -eq 137 ]; then exit $rc; fi
+done
