@@ -27,3 +27,6 @@ if [ "${PROFILE:-0}" = "1" ]; then
         -- python3 bench.py --steps 100 --warmup 5 --no-cpu-baseline "$@"
     find gpurun_out/prof -name "*kernel_stats.csv" -exec cat {} \;
 fi
+for cfg in ${BENCH_CONFIGS:-}; do
+    step "bench_$cfg" 600 python bench.py --config "$cfg" --no-cpu-baseline --steps 50
+done

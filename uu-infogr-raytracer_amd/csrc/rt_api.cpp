@@ -87,6 +87,8 @@ struct Device {
 struct SceneLayout {
     int S = 0, P = 0, L = 0, limit = 0;
     size_t off_sph = 0, off_mat = 0, off_pl = 0, off_li = 0, bytes = 0;
+    bool generic_pow = false;        // a specular material with n not in {0.5, 1, 2}
+    std::vector<DevSphere> host_sph;  // for the per-frame primary constants
 };
 }  // namespace
 
@@ -228,6 +230,14 @@ int view_params(rt_ctx* ctx, int W, int H, LaunchParams& lp) {
     lp.fwd[0] = v.forward.x, lp.fwd[1] = v.forward.y, lp.fwd[2] = v.forward.z;
     lp.pw = v.plane_width, lp.ph = v.plane_height, lp.nearc = v.near_clip;
     lp.W = W, lp.H = H;
+    // primary-segment sphere constants (origin = camera for every pixel)
+    const std::vector<DevSphere>& sph = ctx->layout.host_sph;
+    lp.prim_const = sph.size() <= (size_t)MAX_PRIM_CONST ? 1 : 0;
+    if (lp.prim_const)
+        for (size_t i = 0; i < sph.size(); ++i) {
+            const H3 oc{lp.cam[0] - sph[i].cx, lp.cam[1] - sph[i].cy, lp.cam[2] - sph[i].cz};
+            lp.pc[i] = PrimConst{oc.x, oc.y, oc.z, hdot(oc, oc) - sph[i].r2};
+        }
     return RT_OK;
 }
 
@@ -258,7 +268,7 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
     hipStream_t saved = d.stream;
     d.stream = stream;
     begin_timed(ctx, d, 0);
-    int e = launch_trace(lp, stream);
+    int e = launch_trace(lp, ctx->layout.generic_pow, stream);
     end_timed(d);
     d.stream = saved;
     if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "trace launch failed: %s", hipGetErrorString((hipError_t)e));
@@ -402,6 +412,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
         sph[i] = DevSphere{s.center.x, s.center.y, s.center.z, s.radius * s.radius};  // :336
         mat[i] = dev_material(s.material, ambient);
     }
+    L.host_sph.assign(sph, sph + n_spheres);
     for (int i = 0; i < n_planes; ++i) {
         const rt_plane& p = planes[i];
         const H3 n = h3(p.normal);
@@ -429,6 +440,8 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
         d.a4 = 4.0f * d.a;
         li[i] = d;
     }
+    for (int i = 0; i < n_spheres + n_planes; ++i)
+        if ((mat[i].flags & MAT_SPEC) && mat[i].pow_kind == POW_GENERIC) L.generic_pow = true;
     for (Device& d : ctx->dev) {
         DeviceGuard guard(d.id);
         HIP_TRY(ctx, hipStreamSynchronize(d.stream));

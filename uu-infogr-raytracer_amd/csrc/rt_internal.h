@@ -55,7 +55,16 @@ struct DevLight {
 constexpr int COUNTER_SLOTS = 256;
 constexpr int COUNTER_WORDS = COUNTER_SLOTS * 4;
 
-// Per-launch parameters (passed by value as the kernel argument block).
+// Camera-relative sphere constants of the primary segment (origin = camera position for
+// every pixel): oc = cam - center and c = Dot(oc, oc) - r^2 of IntersectsSphere
+// (RayTracer.cs:614-619), computed once per frame on the host with the same binary32
+// operations and passed in the kernarg block for up to MAX_PRIM_CONST spheres.
+struct PrimConst {
+    float ocx, ocy, ocz, c;
+};
+constexpr int MAX_PRIM_CONST = 64;
+
+// Per-launch parameters (passed by value as the kernel argument block, < 4 KiB).
 struct LaunchParams {
     const DevSphere* sph;
     const DevMaterial* mat;  // [S + P]
@@ -71,10 +80,13 @@ struct LaunchParams {
     int band_rows, band_first, band_step, local_rows;
     int32_t* out;
     unsigned long long* counters;  // COUNTER_SLOTS x {primary, reflect, shadow, pad}
+    int prim_const;                // 1: pc[0..S) valid (S <= MAX_PRIM_CONST)
+    PrimConst pc[MAX_PRIM_CONST];
 };
 
 // Launchers (rt_kernel.hip).  Return hipError_t as int.
-int launch_trace(const LaunchParams& p, void* stream);
+// generic_pow: some material needs the f64 Math.Pow path (exponent not 0.5, 1 or 2).
+int launch_trace(const LaunchParams& p, bool generic_pow, void* stream);
 int launch_scatter_bands(const int32_t* bands, int32_t* frame, int W, int H, int band_rows, int band_first,
                          int band_step, int n_bands, void* stream);
 

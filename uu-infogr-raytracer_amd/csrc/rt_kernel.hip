@@ -7,16 +7,19 @@
 //  * one wave64 lane per pixel; a wave covers an 8x8 pixel tile, a 256-thread workgroup
 //    a 16x16 tile (ray coherence -> fewer divergent primitive hits per wave);
 //  * the scene is tiny (< 6 KB at 64 spheres) and every loop over spheres / planes / lights
-//    is wave-uniform, so primitive data is read with scalar loads (SGPR operands);
+//    is wave-uniform, so primitive data is read with scalar loads (SGPR operands); the
+//    camera-relative sphere constants of the primary segment come in the kernarg block;
 //  * the reference shades EVERY hit primitive and recurses from each mirror hit; only the
 //    nearest (by the reference's own selection rules) reaches the pixel, so each lane walks
 //    a single chain of segments forward (intersection only), pushing one record per
-//    shaded mirror level onto a per-lane stack, then folds colours backward in the
-//    reference's exact order: mirror term, then each light in order, then ambient
+//    shaded hit onto a per-lane stack, then folds colours backward in the reference's
+//    exact order: mirror term, then each light in order, then ambient
 //    (RayTracer.cs:739-778, :850-873).  Bit-identical to the all-hit recursion.
 //  * arithmetic is IEEE binary32 with no FMA contraction (-ffp-contract=off), correctly
 //    rounded '/' and sqrt, IEEE-754-2019 maximum/minimum for .NET Math.Max/Min, f64 where
 //    the reference uses Math.Pow, and .NET's (int) conversion (NaN/overflow -> INT_MIN).
+//  * work the reference does but whose result provably cannot change a selection is
+//    skipped (sqrt/divisions of spheres behind the ray, the far root) -- see root_t1.
 #include <hip/hip_runtime.h>
 
 #include "rt_internal.h"
@@ -54,64 +57,104 @@ __device__ __forceinline__ int32_t net_f2i(float v) {
 // rounding of it equals binary32 x*x); n == 0.5 -> binary32 sqrt (a double result within
 // glibc pow's 0.54 ulp can never straddle a binary32 rounding boundary of sqrt(float):
 // the exact root is >= 2^-49 relative away from every binary32 midpoint).  Other
-// exponents use the device's f64 pow.
+// exponents use the device's f64 pow (compiled in only when the scene needs it).
+template <bool GPOW>
 __device__ __forceinline__ float spec_pow(float x, const DevMaterial& m) {
     switch (m.pow_kind) {
         case POW_ONE: return x;
         case POW_HALF: return __builtin_sqrtf(x);
         case POW_TWO: return x * x;
-        default: return (float)pow((double)x, (double)m.n);
+        default:
+            if constexpr (GPOW) return (float)pow((double)x, (double)m.n);
+            else return x;  // unreachable: the host selects GPOW when any material needs it
     }
 }
 
-// IntersectsSphere, RayTracer.cs:613-642, epsilon 0, for nearest-hit selection.  Returns
-// min(max(t1,0), max(t2,0)) when the discriminant is >= 0, else 0; callers select only
-// t > 0 (primary) / t - 0.01 > 0 (secondary), which is exactly the reference's
-// collision-or-0 distance under either rule.  a4 = 4*a and a2 = 2*a are per-ray.
-__device__ __forceinline__ float sphere_t(f3 o, f3 d, float a2, float a4, const DevSphere& s) {
-    f3 oc = sub(o, mk(s.cx, s.cy, s.cz));
-    float b = 2.0f * dot(oc, d);
-    float c = dot(oc, oc) - s.r2;
-    float disc = b * b - a4 * c;
+// ---------------------------------------------------------------------------------
+// IntersectsSphere (RayTracer.cs:613-642) for nearest-hit selection, epsilon 0.
+//
+// The reference returns dist = min(max(t1,0), max(t2,0)) on a collision (dist > 0) and 0
+// otherwise, with t2 = (-b+sqrt)/2a, t1 = (-b-sqrt)/2a; the callers then select only
+// dist > 0 (TracePixel :977) or dist - 0.01 > 0 (TraceSecondaryRay :804).  When 2a is
+// finite and > 0 (always, for the normalised primary and reflected directions) the
+// exactly-rounded results satisfy t2 >= t1 (numerators ordered, rounding and division by
+// a positive number monotonic), so a selectable distance exists iff t1 > 0, and then it is
+// t1 itself.  t1 > 0 iff fl(-b - sq) > 0 iff -b > sq (gradual underflow), which needs
+// -b > 0 first.  So: no sqrt when b >= 0, no division unless -b > sq, never the t2
+// division.  Returns the reference's distance or 0 (non-selectable) -- identical
+// selections and identical winning distances.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ float root_t1(float b, float disc, float a2) {
+    float t = 0.0f;
+    if (disc >= 0.0f && b < 0.0f) {
+        const float sq = __builtin_sqrtf(disc);  // == (float)Math.Sqrt((double)disc)
+        const float nb = -b;
+        if (nb > sq) t = (nb - sq) / a2;
+    }
+    return t;
+}
+
+// Literal formula, for directions whose 2a is not finite-positive.
+__device__ __forceinline__ float root_full(float b, float disc, float a2) {
     float t = 0.0f;
     if (disc >= 0.0f) {
-        float sq = __builtin_sqrtf(disc);  // == (float)Math.Sqrt((double)disc)
-        float t2 = (-b + sq) / a2;
-        float t1 = (-b - sq) / a2;
+        const float sq = __builtin_sqrtf(disc);
+        const float t2 = (-b + sq) / a2;
+        const float t1 = (-b - sq) / a2;
         t = nmin(nmax0(t1), nmax0(t2));
     }
     return t;
 }
 
-// IntersectsSphere with epsilon 0.001 for the shadow ray of IntersectShadowLight
-// (origin = hit point, direction = light POSITION, RayTracer.cs:574-578).
-__device__ __forceinline__ bool shadow_blocked(f3 hp, const DevLight& l, const DevSphere& s) {
-    f3 oc = sub(hp, mk(s.cx, s.cy, s.cz));
-    f3 lp = mk(l.px, l.py, l.pz);
-    float b = 2.0f * dot(oc, lp);
-    float c = dot(oc, oc) - s.r2;
-    float disc = b * b - l.a4 * c;
+__device__ __forceinline__ float sphere_t(f3 o, f3 d, float a2, float a4, bool a2_ok, const DevSphere& s) {
+    const f3 oc = sub(o, mk(s.cx, s.cy, s.cz));
+    const float b = 2.0f * dot(oc, d);
+    const float c = dot(oc, oc) - s.r2;
+    const float disc = b * b - a4 * c;
+    return a2_ok ? root_t1(b, disc, a2) : root_full(b, disc, a2);
+}
+
+// Shadow ray of IntersectShadowLight (origin = hit point, direction = light POSITION,
+// epsilon 0.001, RayTracer.cs:574-578): collision iff min(max(t1-e,0), max(t2-e,0)) > 0.
+// With 2a finite-positive (uniform per light) and t2 >= t1 that is t1 - e > 0 (and then
+// t2 - e > 0 too), which again needs -b > sq.
+__device__ __forceinline__ bool shadow_blocked(f3 hp, const DevLight& l, bool a2_ok, const DevSphere& s) {
+    const f3 oc = sub(hp, mk(s.cx, s.cy, s.cz));
+    const float b = 2.0f * dot(oc, mk(l.px, l.py, l.pz));
+    const float c = dot(oc, oc) - s.r2;
+    const float disc = b * b - l.a4 * c;
+    if (a2_ok) {
+        if (disc >= 0.0f && b < 0.0f) {
+            const float sq = __builtin_sqrtf(disc);
+            const float nb = -b;
+            if (nb > sq) return (nb - sq) / l.a2 - 0.001f > 0.0f;
+        }
+        return false;
+    }
     if (disc >= 0.0f) {
-        float sq = __builtin_sqrtf(disc);
-        float t2 = (-b + sq) / l.a2;
-        float t1 = (-b - sq) / l.a2;
-        float te = nmin(nmax0(t1 - 0.001f), nmax0(t2 - 0.001f));
-        return te > 0.0f;
+        const float sq = __builtin_sqrtf(disc);
+        const float t2 = (-b + sq) / l.a2;
+        const float t1 = (-b - sq) / l.a2;
+        return nmin(nmax0(t1 - 0.001f), nmax0(t2 - 0.001f)) > 0.0f;
     }
     return false;
 }
 
-// IntersectPlane, RayTracer.cs:590-604: t = (((-o.x*n.x) - o.y*n.y) - o.z*n.z + c.n) / d.n
+// IntersectPlane, RayTracer.cs:590-604: t = (((-o.x*n.x) - o.y*n.y) - o.z*n.z + c.n) / d.n,
+// hit iff t > 0.  The quotient can only be > 0 when numerator and denominator are nonzero
+// with equal signs; otherwise it is <= 0 or NaN (a miss) and the division is skipped.
 __device__ __forceinline__ float plane_t(f3 o, f3 d, const DevPlane& p) {
-    float num = ((-o.x * p.nx - o.y * p.ny) - o.z * p.nz) + p.cn;
-    return num / dot(d, mk(p.nx, p.ny, p.nz));
+    const float num = ((-o.x * p.nx - o.y * p.ny) - o.z * p.nz) + p.cn;
+    const float den = dot(d, mk(p.nx, p.ny, p.nz));
+    return ((num > 0.0f && den > 0.0f) || (num < 0.0f && den < 0.0f)) ? num / den : 0.0f;
 }
 
 // Shading of one shaded hit (TraceSphere :847-873 / TracePlane :736-778): the colour is
 // accumulated in the reference's order -- mirror term (from the deeper segment `sec`),
 // then each light, then ambient.  Returns the colour; adds shadow rays to *n_shadow.
+template <bool GPOW>
 __device__ __forceinline__ f3 shade(const LaunchParams& p, bool is_sphere, int prim, f3 hp, f3 d, float t, f3 sec,
-                                 unsigned* n_shadow) {
+                                    unsigned* n_shadow) {
     const DevMaterial& m = p.mat[is_sphere ? prim : p.S + prim];
     const uint32_t flags = m.flags;
     f3 normal;
@@ -123,8 +166,8 @@ __device__ __forceinline__ f3 shade(const LaunchParams& p, bool is_sphere, int p
         const DevPlane& pl = p.pl[prim];
         normal = mk(pl.nx, pl.ny, pl.nz);
         // checkerboard, :766-770: ((int)u + (int)v) & 1, unchecked int add
-        float u = dot(mk(pl.e1x, pl.e1y, pl.e1z), hp);
-        float v = dot(mk(pl.e2x, pl.e2y, pl.e2z), hp);
+        const float u = dot(mk(pl.e1x, pl.e1y, pl.e1z), hp);
+        const float v = dot(mk(pl.e2x, pl.e2y, pl.e2z), hp);
         tile = (float)(int32_t)(((uint32_t)net_f2i(u) + (uint32_t)net_f2i(v)) & 1u);
     }
     f3 col = mk(0.0f, 0.0f, 0.0f);
@@ -136,16 +179,17 @@ __device__ __forceinline__ f3 shade(const LaunchParams& p, bool is_sphere, int p
         const f3 kd = mk(m.kd[0], m.kd[1], m.kd[2]);
         for (int li = 0; li < p.L; ++li) {
             const DevLight& l = p.li[li];
+            const bool l_ok = l.a2 > 0.0f && l.a2 < __builtin_inff();  // wave-uniform
             bool blocked = false;
-            for (int i = 0; i < p.S && !blocked; ++i) blocked = shadow_blocked(hp, l, p.sph[i]);
+            for (int i = 0; i < p.S && !blocked; ++i) blocked = shadow_blocked(hp, l, l_ok, p.sph[i]);
             const float inten = blocked ? 0.0f : l.intensity;
             // ShapePhongShading, :665-695
             const f3 ldir = normalize(sub(mk(l.px, l.py, l.pz), hp));
             f3 ph = scale(kd, nmax0(dot(normal, ldir)));
             f3 spec = mk(0.0f, 0.0f, 0.0f);
             if (flags & MAT_SPEC) {
-                f3 rs = sub(ldir, scale(normal, 2.0f * dot(ldir, normal)));
-                float sp = spec_pow(nmax0(dot(view, normalize(rs))), m);
+                const f3 rs = sub(ldir, scale(normal, 2.0f * dot(ldir, normal)));
+                const float sp = spec_pow<GPOW>(nmax0(dot(view, normalize(rs))), m);
                 spec = mul(mk(m.ks[0], m.ks[1], m.ks[2]), mk(sp, sp, sp));
             }
             ph = add(ph, spec);
@@ -165,7 +209,7 @@ __device__ __forceinline__ f3 shade(const LaunchParams& p, bool is_sphere, int p
 // ShiftColor, :1046-1052: Math.Clamp (NaN passes), * 255f, Math.Floor, (int), (byte).
 __device__ __forceinline__ uint32_t shift_channel(float c) {
     if (!(c == c)) return 0u;  // NaN -> (int) int.MinValue -> (byte) 0
-    float cl = c < 0.0f ? 0.0f : (c > 1.0f ? 1.0f : c);
+    const float cl = c < 0.0f ? 0.0f : (c > 1.0f ? 1.0f : c);
     return (uint32_t)(int32_t)__builtin_floorf(cl * 255.0f) & 255u;
 }
 
@@ -223,7 +267,68 @@ __device__ __forceinline__ unsigned wave_sum(unsigned v) {
     return v;
 }
 
-template <int K, bool SCRATCH>
+// Nearest hit of one segment.  PRIMARY: TracePixel's rule (:977, :987, :993) and the
+// per-frame camera-relative sphere constants; otherwise TraceSecondaryRay's asymmetric
+// rule (:804-806, :819-821, :825).
+struct Hit {
+    float t;
+    int prim;  // >= 0 sphere, ~plane for planes, or HIT_NONE
+};
+constexpr int HIT_NONE = 0x7fffffff;
+
+template <bool PRIMARY>
+__device__ __forceinline__ Hit nearest(const LaunchParams& p, f3 o, f3 d) {
+    const float a = dot(d, d);
+    const float a2 = 2.0f * a, a4 = 4.0f * a;
+    const bool a2_ok = a2 > 0.0f && a2 < __builtin_inff();
+    float best_s = __builtin_inff();
+    int win_s = -1;
+    if (PRIMARY && p.prim_const) {
+        // o == camera: oc = cam - c and c = oc.oc - r^2 are the same per frame (:614-619)
+#pragma unroll 2
+        for (int i = 0; i < p.S; ++i) {
+            const PrimConst pc = p.pc[i];
+            const float b = 2.0f * dot(mk(pc.ocx, pc.ocy, pc.ocz), d);
+            const float disc = b * b - a4 * pc.c;
+            const float t = a2_ok ? root_t1(b, disc, a2) : root_full(b, disc, a2);
+            if (t > 0.0f && best_s > t) {
+                best_s = t;
+                win_s = i;
+            }
+        }
+    } else {
+#pragma unroll 2
+        for (int i = 0; i < p.S; ++i) {
+            const float t = sphere_t(o, d, a2, a4, a2_ok, p.sph[i]);
+            if (PRIMARY) {
+                if (t > 0.0f && best_s > t) {
+                    best_s = t;
+                    win_s = i;
+                }
+            } else {
+                const float tm = t - 0.01f;
+                if (tm > 0.0f && tm < best_s) {
+                    best_s = t;
+                    win_s = i;
+                }
+            }
+        }
+    }
+    float best_p = __builtin_inff();
+    int win_p = -1;
+    for (int i = 0; i < p.P; ++i) {
+        const float t = plane_t(o, d, p.pl[i]);
+        if (t > 0.0f && t < best_p) {
+            best_p = t;
+            win_p = i;
+        }
+    }
+    if (best_s < best_p) return Hit{best_s, win_s};
+    if (win_p >= 0) return Hit{best_p, ~win_p};
+    return Hit{0.0f, HIT_NONE};
+}
+
+template <int K, bool SCRATCH, bool GPOW>
 __global__ __launch_bounds__(256) void trace_kernel(LaunchParams p) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -241,65 +346,28 @@ __global__ __launch_bounds__(256) void trace_kernel(LaunchParams p) {
         const float px = (float)x / (float)p.W - 0.5f;
         const float py = (float)y / (float)p.H - 0.5f;
         const float lx = px * p.pw, ly = py * p.ph, lz = 1.0f * p.nearc;
-        f3 vp = add(add(add(cam, scale(mk(p.right[0], p.right[1], p.right[2]), lx)),
-                        scale(mk(p.up[0], p.up[1], p.up[2]), ly)),
-                    scale(mk(p.fwd[0], p.fwd[1], p.fwd[2]), lz));
+        const f3 vp = add(add(add(cam, scale(mk(p.right[0], p.right[1], p.right[2]), lx)),
+                              scale(mk(p.up[0], p.up[1], p.up[2]), ly)),
+                          scale(mk(p.fwd[0], p.fwd[1], p.fwd[2]), lz));
         f3 d = normalize(sub(vp, cam));
         f3 o = cam;
 
         LevelStack<K, SCRATCH> stk;
         f3 leaf = mk(0.0f, 0.0f, 0.0f);
+        Hit h = nearest<true>(p, o, d);
         int count = 0;
         for (;;) {
-            const bool primary = count == 0;
-            const float a = dot(d, d);
-            const float a2 = 2.0f * a, a4 = 4.0f * a;
-            // nearest sphere: TracePixel rule (:977) for the primary ray, the asymmetric
-            // TraceSecondaryRay rule (:804-806) for reflected rays
-            float best_s = __builtin_inff();
-            int win_s = -1;
-            for (int i = 0; i < p.S; ++i) {
-                const float t = sphere_t(o, d, a2, a4, p.sph[i]);
-                const float tm = t - 0.01f;
-                const bool sel = primary ? (t > 0.0f && best_s > t) : (tm > 0.0f && tm < best_s);
-                if (sel) {
-                    best_s = t;
-                    win_s = i;
-                }
-            }
-            // nearest plane (:987, :819)
-            float best_p = __builtin_inff();
-            int win_p = -1;
-            for (int i = 0; i < p.P; ++i) {
-                const float t = plane_t(o, d, p.pl[i]);
-                if (t > 0.0f && t < best_p) {
-                    best_p = t;
-                    win_p = i;
-                }
-            }
-            bool is_sphere;
-            float t;
-            int prim;
-            if (best_s < best_p) {  // :993 / :825
-                is_sphere = true;
-                t = best_s;
-                prim = win_s;
-            } else if (win_p >= 0) {
-                is_sphere = false;
-                t = best_p;
-                prim = win_p;
-            } else {
-                break;  // nothing hit: plane colour stays Zero
-            }
-            if (t - 0.01f <= 0.0f) break;  // too close: Zero (:731, :839)
-            if (count > p.limit) {        // terminal segment: Zero / One (:734, :843)
+            if (h.prim == HIT_NONE) break;      // nothing hit: plane colour stays Zero
+            if (h.t - 0.01f <= 0.0f) break;     // too close: Zero (:731, :839)
+            const bool is_sphere = h.prim >= 0;
+            if (count > p.limit) {              // terminal segment: Zero / One (:734, :843)
                 if (!is_sphere) leaf = mk(1.0f, 1.0f, 1.0f);
                 break;
             }
             // shaded hit: record it; mirror hits continue with the reflected segment
-            const f3 hp = add(o, scale(d, t));
-            const int code = is_sphere ? prim : ~prim;
-            stk.push(make_float4(hp.x, hp.y, hp.z, t), make_float4(d.x, d.y, d.z, __int_as_float(code)));
+            const f3 hp = add(o, scale(d, h.t));
+            stk.push(make_float4(hp.x, hp.y, hp.z, h.t), make_float4(d.x, d.y, d.z, __int_as_float(h.prim)));
+            const int prim = is_sphere ? h.prim : ~h.prim;
             const uint32_t flags = p.mat[is_sphere ? prim : p.S + prim].flags;
             if (!(flags & MAT_MIRROR)) break;
             f3 normal;
@@ -314,6 +382,7 @@ __global__ __launch_bounds__(256) void trace_kernel(LaunchParams p) {
             o = hp;
             ++count;
             ++n_refl;
+            h = nearest<false>(p, o, d);
         }
         // backward fold: every recorded hit is shaded in reverse order; a mirror hit
         // consumes the colour of the segment after it (levels 0..limit push at most one
@@ -324,8 +393,8 @@ __global__ __launch_bounds__(256) void trace_kernel(LaunchParams p) {
             stk.pop(ra, rb);
             const int code = __float_as_int(rb.w);
             const bool is_s = code >= 0;
-            col = shade(p, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z), ra.w, col,
-                        &n_shadow);
+            col = shade<GPOW>(p, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z), ra.w, col,
+                              &n_shadow);
         }
         const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
         p.out[(size_t)r * (size_t)p.W + (size_t)x] = (int32_t)px32;
@@ -362,22 +431,32 @@ __global__ __launch_bounds__(256) void scatter_bands_kernel(const int32_t* __res
     }
 }
 
-int launch_trace(const LaunchParams& p, void* stream) {
+template <bool GPOW>
+static void launch_variant(const LaunchParams& p, dim3 grid, dim3 block, hipStream_t s) {
+    const int need = p.limit + 1;  // levels 0..limit can push a record
+    if (need <= 1)
+        hipLaunchKernelGGL((trace_kernel<1, false, GPOW>), grid, block, 0, s, p);
+    else if (need <= 2)
+        hipLaunchKernelGGL((trace_kernel<2, false, GPOW>), grid, block, 0, s, p);
+    else if (need <= 4)
+        hipLaunchKernelGGL((trace_kernel<4, false, GPOW>), grid, block, 0, s, p);
+    else if (need <= 6)
+        hipLaunchKernelGGL((trace_kernel<6, false, GPOW>), grid, block, 0, s, p);
+    else if (need <= 8)
+        hipLaunchKernelGGL((trace_kernel<8, false, GPOW>), grid, block, 0, s, p);
+    else
+        hipLaunchKernelGGL((trace_kernel<64, true, GPOW>), grid, block, 0, s, p);
+}
+
+int launch_trace(const LaunchParams& p, bool generic_pow, void* stream) {
     if (p.local_rows <= 0 || p.W <= 0) return (int)hipSuccess;
     const dim3 grid((unsigned)((p.W + 15) / 16), (unsigned)((p.local_rows + 15) / 16));
     const dim3 block(256);
     hipStream_t s = (hipStream_t)stream;
-    const int need = p.limit + 1;  // levels 0..limit can push a mirror record
-    if (need <= 1)
-        hipLaunchKernelGGL((trace_kernel<1, false>), grid, block, 0, s, p);
-    else if (need <= 2)
-        hipLaunchKernelGGL((trace_kernel<2, false>), grid, block, 0, s, p);
-    else if (need <= 4)
-        hipLaunchKernelGGL((trace_kernel<4, false>), grid, block, 0, s, p);
-    else if (need <= 8)
-        hipLaunchKernelGGL((trace_kernel<8, false>), grid, block, 0, s, p);
+    if (generic_pow)
+        launch_variant<true>(p, grid, block, s);
     else
-        hipLaunchKernelGGL((trace_kernel<64, true>), grid, block, 0, s, p);
+        launch_variant<false>(p, grid, block, s);
     return (int)hipGetLastError();
 }
 
