@@ -101,7 +101,7 @@ def main():
     import torch
     import torch.distributed as dist
 
-    from raytracer_hip import Context, abi, bands_of, scenes
+    from raytracer_hip import Context, abi, scenes
     if not os.path.exists(abi.LIB_PATH):
         subprocess.run(["make", "-s", "-C", os.path.join(PKG, "csrc")], check=True)
 
@@ -124,19 +124,19 @@ def main():
         def step():
             ctx.render_device(W, H, frame.data_ptr(), s)
     else:
-        br = args.band_rows
-        max_nb = bands_of(H, br, 0, world)
-        local_buf = torch.zeros(max_nb * br * W, dtype=torch.int32, device="cuda")
-        px_per_launch = bands_of(H, br, rank, world) * br * W
-        gather_list = [torch.empty_like(local_buf) for _ in range(world)] if rank == 0 else None
+        from raytracer_hip.dist import BandGather, RowBands
+        rb = RowBands(W, H, args.band_rows, rank, world)
+        bg = BandGather(rb, torch.device("cuda", local))
+        px_per_launch = rb.pixels
         frame = torch.empty(W * H, dtype=torch.int32, device="cuda") if rank == 0 else None
 
         def step():
-            ctx.render_bands(W, H, br, rank, world, local_buf.data_ptr(), s)
-            dist.gather(local_buf, gather_list, dst=0)
+            # trace this rank's bands -> RCCL gather of the slots to rank 0 -> reassemble there
+            ctx.render_bands(W, H, rb.band_rows, rank, world, bg.local.data_ptr(), s)
+            parts = bg.gather()
             if rank == 0:
                 for r in range(world):
-                    ctx.scatter_bands(W, H, br, r, world, gather_list[r].data_ptr(), frame.data_ptr(), s)
+                    ctx.scatter_bands(W, H, rb.band_rows, r, world, parts[r].data_ptr(), frame.data_ptr(), s)
 
     for _ in range(args.warmup):
         step()

@@ -1,0 +1,46 @@
+"""Worker for the multi-process (gloo, CPU) tests of raytracer_hip.dist.
+
+Each rank traces only its own interleaved row bands -- with the CPU oracle standing in for
+rt_render_bands, since there is no GPU here -- packs them into its slot, the slots are
+gathered to rank 0 with torch.distributed (gloo), and rank 0 reassembles the frame with the
+host mirror of rt_scatter_bands and compares it with the oracle's full frame.
+"""
+import os
+import sys
+
+
+def run(rank, world, port, cfg, width, height, band_rows, result_path):
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path[:0] = [os.path.join(root, "uu-infogr-raytracer_amd"), os.path.join(root, "oracle"), here]
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import pyoracle
+    from raytracer_hip import scenes
+    from raytracer_hip.dist import BandGather, RowBands, scatter_host
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        sc = scenes.config(cfg).resized(width, height)
+        rb = RowBands(width, height, band_rows, rank, world)
+        g = BandGather(rb, "cpu")
+        local = g.local.numpy().reshape(-1, width)
+        for l0, y0, n in rb.row_spans():
+            rows, _ = pyoracle.render(sc, pyoracle.MODE_NEAREST, 2, rows=(y0, y0 + n))
+            local[l0:l0 + n] = rows
+        parts = g.gather()
+        ok = torch.tensor([1], dtype=torch.int32)
+        if rank == 0:
+            frame = scatter_host([p.numpy() for p in parts], width, height, band_rows)
+            full, _ = pyoracle.render(sc, pyoracle.MODE_NEAREST, 2)
+            same = bool(np.array_equal(frame, full))
+            ok[0] = int(same)
+            with open(result_path, "w") as f:
+                f.write("ok" if same else f"mismatch {int((frame != full).sum())}")
+        dist.broadcast(ok, 0)
+        assert ok.item() == 1
+    finally:
+        dist.destroy_process_group()

@@ -18,9 +18,10 @@ import numpy as np
 
 from . import abi, scenes
 from .abi import RayTracerError, check, load_library
+from .dist import bands_of
 
 __all__ = ["Surface", "RayTracer", "Context", "RayTracerError", "scenes", "abi", "load_library",
-           "device_count", "camera_view"]
+           "device_count", "camera_view", "bands_of"]
 
 
 def device_count() -> int:
@@ -137,12 +138,6 @@ class Context:
 
     def reset_stats(self):
         self._check(self.lib.rt_reset_stats(self.ptr))
-
-
-def bands_of(height: int, band_rows: int, first: int, step: int) -> int:
-    """Number of row bands b = first, first+step, ... with b*band_rows < height."""
-    total = (height + band_rows - 1) // band_rows
-    return (total - 1 - first) // step + 1 if first < total else 0
 
 
 class RayTracer:

@@ -1,0 +1,77 @@
+"""Row-band sharding of a frame across ranks (one process per GPU), SURVEY.md 8(e).
+
+Pixels are independent, so a frame is split into interleaved bands of `band_rows` rows:
+band b goes to rank b % world (sky rows are nearly free, contiguous tiles would be badly
+imbalanced).  Each rank traces its bands packed one after the other into a slot of
+`max_bands * band_rows * W` int32 (ranks with one band fewer leave the tail of the slot
+unused), the slots are gathered to rank 0 -- torch.distributed backend "nccl" is RCCL on
+ROCm, point-to-point over xGMI -- and rank 0 scatters each slot back into the row-major
+frame (rt_scatter_bands on the GPU; `scatter_host` below is its host mirror).
+
+The same code runs under backend "gloo" on CPU tensors for the multi-process tests.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+
+def bands_of(height: int, band_rows: int, first: int, step: int) -> int:
+    """Number of bands b = first, first+step, ... with b*band_rows < height."""
+    total = (height + band_rows - 1) // band_rows
+    return (total - 1 - first) // step + 1 if first < total else 0
+
+
+class RowBands:
+    """This rank's share of a W x H frame."""
+
+    def __init__(self, width: int, height: int, band_rows: int, rank: int, world: int):
+        if band_rows <= 0 or world <= 0 or not 0 <= rank < world:
+            raise ValueError("bad band layout")
+        self.width, self.height, self.band_rows = width, height, band_rows
+        self.rank, self.world = rank, world
+        self.n_bands = bands_of(height, band_rows, rank, world)
+        self.max_bands = bands_of(height, band_rows, 0, world)
+        self.slot_elems = max(1, self.max_bands) * band_rows * width
+        self.pixels = self.n_bands * band_rows * width  # traced by this rank (incl. rows past H)
+
+    def global_row(self, local_row: int) -> int:
+        """Frame row of packed local row `local_row` (may be >= height in the last band)."""
+        band = self.rank + (local_row // self.band_rows) * self.world
+        return band * self.band_rows + local_row % self.band_rows
+
+    def row_spans(self):
+        """[(local_row0, frame_row0, n_rows)] of every band of this rank, clipped to the frame."""
+        out = []
+        for k in range(self.n_bands):
+            y0 = (self.rank + k * self.world) * self.band_rows
+            n = min(self.band_rows, self.height - y0)
+            out.append((k * self.band_rows, y0, n))
+        return out
+
+
+def scatter_host(parts, width: int, height: int, band_rows: int) -> np.ndarray:
+    """Host mirror of rt_scatter_bands for every rank's gathered slot (rank order)."""
+    world = len(parts)
+    frame = np.full((height, width), -1, dtype=np.int32)
+    for rank, part in enumerate(parts):
+        rb = RowBands(width, height, band_rows, rank, world)
+        img = np.asarray(part).reshape(-1, width)
+        for l0, y0, n in rb.row_spans():
+            frame[y0:y0 + n] = img[l0:l0 + n]
+    return frame
+
+
+class BandGather:
+    """Gather of every rank's band slot to rank 0 (torch.distributed, RCCL on ROCm GPUs)."""
+
+    def __init__(self, rb: RowBands, device, dtype=None):
+        import torch
+        self.rb = rb
+        dtype = dtype or torch.int32
+        self.local = torch.zeros(rb.slot_elems, dtype=dtype, device=device)
+        self.parts = [torch.empty_like(self.local) for _ in range(rb.world)] if rb.rank == 0 else None
+
+    def gather(self):
+        import torch.distributed as dist
+        dist.gather(self.local, self.parts, dst=0)
+        return self.parts
