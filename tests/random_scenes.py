@@ -42,13 +42,15 @@ def _material(rng):
     return Material((0.0, 0.0, 0.0), _color(rng), (0.0, 0.0, 0.0), 0.0, (0.0, 0.0, 0.0))  # ambient only
 
 
-def random_scene(seed: int, width: int = 96, height: int = 64) -> Scene:
+def random_scene(seed: int, width: int = 96, height: int = 64, dense: bool = False) -> Scene:
+    """dense=True: 12-100 smaller spheres -- exercises the wave-bundle culling path
+    (CULL_MIN_SPHERES = 12) and its 64-sphere chunking."""
     rng = np.random.default_rng(seed)
-    ns = int(rng.integers(0, 12))
+    ns = int(rng.integers(12, 101)) if dense else int(rng.integers(0, 12))
     spheres = []
     for _ in range(ns):
-        r = float(f32(rng.uniform(0.2, 2.0)))
-        spheres.append(Sphere(_v(rng, -6, 6)[:2] + (float(f32(rng.uniform(2, 20))),), r, _material(rng)))
+        r = float(f32(rng.uniform(0.05, 0.9) if dense else rng.uniform(0.2, 2.0)))
+        spheres.append(Sphere(_v(rng, -6, 6)[:2] + (float(f32(rng.uniform(1, 24))),), r, _material(rng)))
     planes = []
     for _ in range(int(rng.integers(0, 3))):
         kind = rng.integers(0, 4)

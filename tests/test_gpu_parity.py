@@ -73,6 +73,17 @@ def test_random_scenes_vs_oracle(gpu_ctx, oracle, seed):
     assert ray_counts(st) == {k: ost[k] for k in ("primary_rays", "reflect_rays", "shadow_rays")}
 
 
+@pytest.mark.parametrize("seed", list(range(100, 130)))
+def test_dense_random_scenes_vs_oracle(gpu_ctx, oracle, seed):
+    """12-100 spheres: the wave-bundle culling path, 64-sphere mask chunks."""
+    import random_scenes
+    sc = random_scenes.random_scene(seed, 128, 96, dense=True)
+    px, st = render_gpu(gpu_ctx, sc)
+    want, ost = oracle.render(sc, oracle.MODE_NEAREST, 4)
+    assert_same(px, want, sc.name)
+    assert ray_counts(st) == {k: ost[k] for k in ("primary_rays", "reflect_rays", "shadow_rays")}
+
+
 @pytest.mark.parametrize("w,h", [(1, 1), (17, 13), (15, 16), (16, 15), (33, 65), (1000, 3)])
 def test_ragged_frame_sizes(gpu_ctx, oracle, w, h):
     sc = scenes.config("C3").resized(w, h)

@@ -147,3 +147,13 @@ def test_random_scenes_oracle_vs_emulation(oracle, seed):
     with np.errstate(all="ignore"):
         emu = emu_f32.Emu(sc).render()
     assert np.array_equal(ref, near) and np.array_equal(ref, emu)
+
+
+@pytest.mark.parametrize("seed", [100, 107, 115])
+def test_dense_random_scenes_oracle_drivers(oracle, seed):
+    """Dense scenes (the GPU culling path's inputs): all-hit and nearest-hit drivers agree."""
+    import random_scenes
+    sc = random_scenes.random_scene(seed, 64, 48, dense=True)
+    ref, _ = oracle.render(sc, oracle.MODE_REFERENCE, 4)
+    near, _ = oracle.render(sc, oracle.MODE_NEAREST, 4)
+    assert np.array_equal(ref, near)

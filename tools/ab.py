@@ -1,0 +1,64 @@
+"""Interleaved A/B timing of two builds of libraytracer_hip in ONE process (guide rule 24).
+
+    python tools/ab.py LIB_A LIB_B [--config C2] [--rounds 10] [--frames 50]
+
+Each round renders `frames` frames with A then B (order alternating per round); the
+library's own HIP-event kernel times are compared (median and min per frame)."""
+import argparse
+import ctypes as C
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "uu-infogr-raytracer_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs=2)
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--rounds", type=int, default=10)
+    ap.add_argument("--frames", type=int, default=50)
+    a = ap.parse_args()
+    import torch
+    from raytracer_hip import abi, scenes
+    torch.cuda.set_device(0)
+    sc = scenes.config(a.config)
+    W, H = sc.width, sc.height
+    out = torch.empty(W * H, dtype=torch.int32, device="cuda")
+    ctxs, libs = [], []
+    for path in a.libs:
+        lib = abi.load_library(os.path.abspath(path), local=True)
+        ctx = C.c_void_p()
+        assert lib.rt_create(1, C.byref(ctx)) == 0, lib.rt_last_error(None)
+        S, P, L = sc.c_arrays()
+        assert lib.rt_set_scene(ctx, S, len(sc.spheres), P, len(sc.planes), L, len(sc.lights),
+                                abi.rt_vec3(*sc.ambient), sc.recursion_limit) == 0
+        assert lib.rt_set_camera(ctx, C.byref(sc.c_camera())) == 0
+        libs.append(lib)
+        ctxs.append(ctx)
+    frames = {0: [], 1: []}
+    crcs = {}
+    import zlib
+    for rnd in range(a.rounds + 1):
+        order = (0, 1) if rnd % 2 == 0 else (1, 0)
+        for i in order:
+            lib, ctx = libs[i], ctxs[i]
+            lib.rt_reset_stats(ctx)
+            for _ in range(a.frames):
+                assert lib.rt_render_device(ctx, W, H, C.c_void_p(out.data_ptr()), None) == 0
+            st = abi.rt_stats()
+            lib.rt_get_stats(ctx, C.byref(st))
+            if rnd > 0:  # round 0 = warm-up
+                frames[i].append(st.kernel_ms / st.launches)
+            crcs[i] = zlib.crc32(out.cpu().numpy().tobytes())
+    for i in (0, 1):
+        v = frames[i]
+        print(f"{os.path.basename(a.libs[i]):32s} {a.config}: median {statistics.median(v)*1e3:8.2f} us  "
+              f"min {min(v)*1e3:8.2f} us  crc {crcs[i]:08x}")
+    print(f"B/A median ratio {statistics.median(frames[1]) / statistics.median(frames[0]):.3f}")
+
+
+if __name__ == "__main__":
+    main()

@@ -16,7 +16,7 @@ for group in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_
     i=$((i+1))
     echo "== pass $i: $group"
     timeout -k 10 300 rocprofv3 --pmc $group --output-format csv -d "$OUT/p$i" -o run \
-        -- python3 bench.py --config "$CFG" --steps 20 --warmup 2 --no-cpu-baseline "$@" > "$OUT/p$i.log" 2>&1
+        -- python3 bench.py --config "$CFG" --steps ${PMC_STEPS:-20} --warmup 2 --no-cpu-baseline "$@" > "$OUT/p$i.log" 2>&1
     rc=$?
     echo "rc=$rc"
     if [ $rc -ne 0 ] && grep -qiE "memory access fault|segmentation|core dumped" "$OUT/p$i.log"; then exit $rc; fi

@@ -149,63 +149,6 @@ __device__ __forceinline__ float plane_t(f3 o, f3 d, const DevPlane& p) {
     return ((num > 0.0f && den > 0.0f) || (num < 0.0f && den < 0.0f)) ? num / den : 0.0f;
 }
 
-// Shading of one shaded hit (TraceSphere :847-873 / TracePlane :736-778): the colour is
-// accumulated in the reference's order -- mirror term (from the deeper segment `sec`),
-// then each light, then ambient.  Returns the colour; adds shadow rays to *n_shadow.
-template <bool GPOW>
-__device__ __forceinline__ f3 shade(const LaunchParams& p, bool is_sphere, int prim, f3 hp, f3 d, float t, f3 sec,
-                                    unsigned* n_shadow) {
-    const DevMaterial& m = p.mat[is_sphere ? prim : p.S + prim];
-    const uint32_t flags = m.flags;
-    f3 normal;
-    float tile = 1.0f;
-    if (is_sphere) {
-        const DevSphere& s = p.sph[prim];
-        normal = normalize(sub(hp, mk(s.cx, s.cy, s.cz)));  // SpherePhongShading :706
-    } else {
-        const DevPlane& pl = p.pl[prim];
-        normal = mk(pl.nx, pl.ny, pl.nz);
-        // checkerboard, :766-770: ((int)u + (int)v) & 1, unchecked int add
-        const float u = dot(mk(pl.e1x, pl.e1y, pl.e1z), hp);
-        const float v = dot(mk(pl.e2x, pl.e2y, pl.e2z), hp);
-        tile = (float)(int32_t)(((uint32_t)net_f2i(u) + (uint32_t)net_f2i(v)) & 1u);
-    }
-    f3 col = mk(0.0f, 0.0f, 0.0f);
-    if (flags & MAT_MIRROR) col = add(col, mul(sec, mk(m.km[0], m.km[1], m.km[2])));
-    if (flags & MAT_DIFFUSE) {
-        const f3 view = normalize(d);  // ShapePhongShading :668 (not negated)
-        // sphere: (1 / t) * t (:866);  plane: (float)(1 / Math.Pow(t, 2)) (:754), exact as 1/(t*t) in f64
-        const float att = is_sphere ? (1.0f / t) * t : (float)(1.0 / ((double)t * (double)t));
-        const f3 kd = mk(m.kd[0], m.kd[1], m.kd[2]);
-        for (int li = 0; li < p.L; ++li) {
-            const DevLight& l = p.li[li];
-            const bool l_ok = l.a2 > 0.0f && l.a2 < __builtin_inff();  // wave-uniform
-            bool blocked = false;
-            for (int i = 0; i < p.S && !blocked; ++i) blocked = shadow_blocked(hp, l, l_ok, p.sph[i]);
-            const float inten = blocked ? 0.0f : l.intensity;
-            // ShapePhongShading, :665-695
-            const f3 ldir = normalize(sub(mk(l.px, l.py, l.pz), hp));
-            f3 ph = scale(kd, nmax0(dot(normal, ldir)));
-            f3 spec = mk(0.0f, 0.0f, 0.0f);
-            if (flags & MAT_SPEC) {
-                const f3 rs = sub(ldir, scale(normal, 2.0f * dot(ldir, normal)));
-                const float sp = spec_pow<GPOW>(nmax0(dot(view, normalize(rs))), m);
-                spec = mul(mk(m.ks[0], m.ks[1], m.ks[2]), mk(sp, sp, sp));
-            }
-            ph = add(ph, spec);
-            const float ia = inten * att;
-            f3 term = mul(mk(ia, ia, ia), ph);
-            if (!is_sphere) {
-                term = mul(term, mk(tile, tile, tile));
-                term = mk(nmax0(term.x), nmax0(term.y), nmax0(term.z));  // .Max(0f), :775
-            }
-            col = add(col, term);
-        }
-        *n_shadow += (unsigned)p.L;
-    }
-    return add(col, mk(m.amb[0], m.amb[1], m.amb[2]));
-}
-
 // ShiftColor, :1046-1052: Math.Clamp (NaN passes), * 255f, Math.Floor, (int), (byte).
 __device__ __forceinline__ uint32_t shift_channel(float c) {
     if (!(c == c)) return 0u;  // NaN -> (int) int.MinValue -> (byte) 0
@@ -267,17 +210,73 @@ __device__ __forceinline__ unsigned wave_sum(unsigned v) {
     return v;
 }
 
-// Nearest hit of one segment.  PRIMARY: TracePixel's rule (:977, :987, :993) and the
-// per-frame camera-relative sphere constants; otherwise TraceSecondaryRay's asymmetric
-// rule (:804-806, :819-821, :825).
+// Result of a nearest-hit search.
 struct Hit {
     float t;
     int prim;  // >= 0 sphere, ~plane for planes, or HIT_NONE
 };
 constexpr int HIT_NONE = 0x7fffffff;
 
+// DIRECT path (scenes with < CULL_MIN_SPHERES spheres): per-lane divergent loops.
+// Shading of one shaded hit (TraceSphere :847-873 / TracePlane :736-778): the colour is
+// accumulated in the reference's order -- mirror term (from the deeper segment `sec`),
+// then each light, then ambient.  Returns the colour; adds shadow rays to *n_shadow.
+template <bool GPOW>
+__device__ __forceinline__ f3 shade_direct(const LaunchParams& p, bool is_sphere, int prim, f3 hp, f3 d, float t, f3 sec,
+                                    unsigned* n_shadow) {
+    const DevMaterial& m = p.mat[is_sphere ? prim : p.S + prim];
+    const uint32_t flags = m.flags;
+    f3 normal;
+    float tile = 1.0f;
+    if (is_sphere) {
+        const DevSphere& s = p.sph[prim];
+        normal = normalize(sub(hp, mk(s.cx, s.cy, s.cz)));  // SpherePhongShading :706
+    } else {
+        const DevPlane& pl = p.pl[prim];
+        normal = mk(pl.nx, pl.ny, pl.nz);
+        // checkerboard, :766-770: ((int)u + (int)v) & 1, unchecked int add
+        const float u = dot(mk(pl.e1x, pl.e1y, pl.e1z), hp);
+        const float v = dot(mk(pl.e2x, pl.e2y, pl.e2z), hp);
+        tile = (float)(int32_t)(((uint32_t)net_f2i(u) + (uint32_t)net_f2i(v)) & 1u);
+    }
+    f3 col = mk(0.0f, 0.0f, 0.0f);
+    if (flags & MAT_MIRROR) col = add(col, mul(sec, mk(m.km[0], m.km[1], m.km[2])));
+    if (flags & MAT_DIFFUSE) {
+        const f3 view = normalize(d);  // ShapePhongShading :668 (not negated)
+        // sphere: (1 / t) * t (:866);  plane: (float)(1 / Math.Pow(t, 2)) (:754), exact as 1/(t*t) in f64
+        const float att = is_sphere ? (1.0f / t) * t : (float)(1.0 / ((double)t * (double)t));
+        const f3 kd = mk(m.kd[0], m.kd[1], m.kd[2]);
+        for (int li = 0; li < p.L; ++li) {
+            const DevLight& l = p.li[li];
+            const bool l_ok = l.a2 > 0.0f && l.a2 < __builtin_inff();  // wave-uniform
+            bool blocked = false;
+            for (int i = 0; i < p.S && !blocked; ++i) blocked = shadow_blocked(hp, l, l_ok, p.sph[i]);
+            const float inten = blocked ? 0.0f : l.intensity;
+            // ShapePhongShading, :665-695
+            const f3 ldir = normalize(sub(mk(l.px, l.py, l.pz), hp));
+            f3 ph = scale(kd, nmax0(dot(normal, ldir)));
+            f3 spec = mk(0.0f, 0.0f, 0.0f);
+            if (flags & MAT_SPEC) {
+                const f3 rs = sub(ldir, scale(normal, 2.0f * dot(ldir, normal)));
+                const float sp = spec_pow<GPOW>(nmax0(dot(view, normalize(rs))), m);
+                spec = mul(mk(m.ks[0], m.ks[1], m.ks[2]), mk(sp, sp, sp));
+            }
+            ph = add(ph, spec);
+            const float ia = inten * att;
+            f3 term = mul(mk(ia, ia, ia), ph);
+            if (!is_sphere) {
+                term = mul(term, mk(tile, tile, tile));
+                term = mk(nmax0(term.x), nmax0(term.y), nmax0(term.z));  // .Max(0f), :775
+            }
+            col = add(col, term);
+        }
+        *n_shadow += (unsigned)p.L;
+    }
+    return add(col, mk(m.amb[0], m.amb[1], m.amb[2]));
+}
+
 template <bool PRIMARY>
-__device__ __forceinline__ Hit nearest(const LaunchParams& p, f3 o, f3 d) {
+__device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d) {
     const float a = dot(d, d);
     const float a2 = 2.0f * a, a4 = 4.0f * a;
     const bool a2_ok = a2 > 0.0f && a2 < __builtin_inff();
@@ -328,8 +327,9 @@ __device__ __forceinline__ Hit nearest(const LaunchParams& p, f3 o, f3 d) {
     return Hit{0.0f, HIT_NONE};
 }
 
+// DIRECT kernel: each lane walks its own chain with per-lane (divergent) control flow.
 template <int K, bool SCRATCH, bool GPOW>
-__global__ __launch_bounds__(256) void trace_kernel(LaunchParams p) {
+__global__ __launch_bounds__(256) void trace_direct_kernel(LaunchParams p) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
@@ -354,7 +354,7 @@ __global__ __launch_bounds__(256) void trace_kernel(LaunchParams p) {
 
         LevelStack<K, SCRATCH> stk;
         f3 leaf = mk(0.0f, 0.0f, 0.0f);
-        Hit h = nearest<true>(p, o, d);
+        Hit h = nearest_direct<true>(p, o, d);
         int count = 0;
         for (;;) {
             if (h.prim == HIT_NONE) break;      // nothing hit: plane colour stays Zero
@@ -382,7 +382,7 @@ __global__ __launch_bounds__(256) void trace_kernel(LaunchParams p) {
             o = hp;
             ++count;
             ++n_refl;
-            h = nearest<false>(p, o, d);
+            h = nearest_direct<false>(p, o, d);
         }
         // backward fold: every recorded hit is shaded in reverse order; a mirror hit
         // consumes the colour of the segment after it (levels 0..limit push at most one
@@ -393,9 +393,384 @@ __global__ __launch_bounds__(256) void trace_kernel(LaunchParams p) {
             stk.pop(ra, rb);
             const int code = __float_as_int(rb.w);
             const bool is_s = code >= 0;
-            col = shade<GPOW>(p, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z), ra.w, col,
+            col = shade_direct<GPOW>(p, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z), ra.w, col,
                               &n_shadow);
         }
+        const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
+        p.out[(size_t)r * (size_t)p.W + (size_t)x] = (int32_t)px32;
+    }
+
+    // work counters: wave sums -> LDS -> one workgroup total added to a spread slot
+    __shared__ unsigned red[4][3];
+    n_prim = wave_sum(n_prim);
+    n_refl = wave_sum(n_refl);
+    n_shadow = wave_sum(n_shadow);
+    if (lane == 0) {
+        red[wave][0] = n_prim;
+        red[wave][1] = n_refl;
+        red[wave][2] = n_shadow;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const unsigned v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+        const unsigned slot = (blockIdx.y * gridDim.x + blockIdx.x) % COUNTER_SLOTS;
+        if (v) atomicAdd(&p.counters[slot * 4 + threadIdx.x], (unsigned long long)v);
+    }
+}
+
+// ---------------------------------------------------------------------------------
+// Wave-level ray bundles and conservative sphere culling.
+//
+// A wave's active rays (origins o_l, directions d_l) are bounded by a reference origin O,
+// an origin radius R >= max |o_l - O|, a unit axis A and a direction spread
+// delta >= max |d_l/|d_l| - A|.  Lane i tests sphere i against the bundle and a ballot
+// gives the wave's candidate mask; the exact per-lane tests then visit only candidates,
+// in ascending sphere index (so the reference's tie rules are untouched).
+//
+// Exactness: a sphere is culled only when, for EVERY lane, the binary32 evaluation of
+// IntersectsSphere provably yields disc < 0 or b >= 0 -- both make the reference's
+// distance non-selectable (root_t1).  With u = o - C and a = d.d, a first-order error
+// analysis of disc = fl(fl(b*b) - fl(fl(4a)*fl(fl(u.u) - r^2))) bounds its error by
+// 4a(14 eps |u|^2 + 4 eps r^2) (eps = 2^-24), so disc < 0 whenever the exact
+// line-to-centre distance D satisfies D >= r (1 + 3 eps) + 9.2e-4 |u|; b >= 0 whenever
+// u.d/|d| >= 4 eps |u|.  The cull demands D >= r (1 + 2^-8) + 2^-8 (|C - O| + R) and
+// u.A >= 2^-8 (|C - O| + R) after subtracting the bundle slack (R, delta terms) --
+// a 4x margin over the analysis, far above the rounding of the cull arithmetic itself.
+// Culling is disabled for a wave when any active lane has a = d.d outside [0.5, 2]
+// (trace rays) or the light's a outside [2^-40, 2^40] (shadow rays), or for spheres
+// with r^2 < 2^-100 or |C - O| outside [2^-30, 2^40] (no underflow/overflow).
+// ---------------------------------------------------------------------------------
+struct Bundle {
+    f3 O, A;
+    float R, delta;
+    bool ok;   // culling allowed
+    bool any;  // some lane active
+};
+
+__device__ __forceinline__ float readlane_f(float v, int lane) {
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+__device__ __forceinline__ f3 readlane3(f3 v, int lane) {
+    return mk(readlane_f(v.x, lane), readlane_f(v.y, lane), readlane_f(v.z, lane));
+}
+// Wave-uniform maximum of a non-negative float (all 64 lanes active): DPP row rotations
+// give each 16-lane row its maximum, four readlanes and integer max (bit patterns of
+// non-negative floats order like the floats; a NaN pattern compares above +inf) finish it.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float wave_max(float v) {
+    v = fmaxf(v, dpp_f<0x121>(v));  // row_ror:1
+    v = fmaxf(v, dpp_f<0x122>(v));  // row_ror:2
+    v = fmaxf(v, dpp_f<0x124>(v));  // row_ror:4
+    v = fmaxf(v, dpp_f<0x128>(v));  // row_ror:8
+    const unsigned a = (unsigned)__builtin_amdgcn_readlane(__float_as_int(v), 0);
+    const unsigned b = (unsigned)__builtin_amdgcn_readlane(__float_as_int(v), 16);
+    const unsigned c = (unsigned)__builtin_amdgcn_readlane(__float_as_int(v), 32);
+    const unsigned d = (unsigned)__builtin_amdgcn_readlane(__float_as_int(v), 48);
+    return __uint_as_float(max(max(a, b), max(c, d)));
+}
+__device__ __forceinline__ float len3(f3 v) { return __builtin_sqrtf(dot(v, v)); }
+__device__ __forceinline__ f3 cross3(f3 l, f3 r) {
+    return mk(l.y * r.z - l.z * r.y, l.z * r.x - l.x * r.z, l.x * r.y - l.y * r.x);
+}
+
+// Converged call (all 64 lanes).  `dir_uniform`: every lane's direction is `d` itself
+// (shadow rays: the light position), so delta = 0.
+__device__ __forceinline__ Bundle make_bundle(f3 o, f3 d, bool active, bool dir_uniform) {
+    Bundle B;
+    const unsigned long long m = __builtin_amdgcn_ballot_w64(active);
+    B.any = m != 0;
+    if (m == 0) {
+        B.ok = false;
+        B.O = o;
+        B.A = d;
+        B.R = B.delta = 0.0f;
+        return B;
+    }
+    const int ref = __builtin_ctzll(m);
+    B.O = readlane3(o, ref);
+    const f3 dref = readlane3(d, ref);
+    B.A = normalize(dref);
+    float e = 0.0f, f = 0.0f;
+    bool bad = false;
+    if (active) {
+        e = len3(sub(o, B.O));
+        bad = !(e < 0x1p40f);  // also NaN / inf origins
+        if (!dir_uniform) {
+            const float a = dot(d, d);
+            f = len3(sub(normalize(d), B.A));
+            bad = bad || !(a >= 0.5f && a <= 2.0f) || !(f < 2.0f);
+        }
+    }
+    const float R = wave_max(e);
+    const float delta = dir_uniform ? 0.0f : wave_max(f);
+    bad = __builtin_amdgcn_ballot_w64(bad) != 0;
+    B.R = R * (1.0f + 0x1p-10f) + 0x1p-60f;
+    B.delta = dir_uniform ? 0.0f : delta * (1.0f + 0x1p-10f) + 0x1p-20f;
+    B.ok = !bad && R < 0x1p40f && B.delta < 0.5f;
+    return B;
+}
+
+// Candidate mask of spheres [base, base+n) (n <= 64) for bundle B.  Converged call.
+__device__ __forceinline__ unsigned long long cull_mask(const LaunchParams& p, const Bundle& B, int base, int n) {
+    const int lane = threadIdx.x & 63;
+    bool cand = false;
+    if (lane < n) {
+        cand = true;
+        if (B.ok) {
+            const DevSphere s = p.sph[base + lane];
+            const f3 w = sub(mk(s.cx, s.cy, s.cz), B.O);
+            const float dc = len3(w);
+            if (s.r2 >= 0x1p-100f && dc >= 0x1p-30f && dc < 0x1p40f) {
+                const float rr = __builtin_sqrtf(s.r2) * (1.0f + 0x1p-8f);
+                const float mgn = 0x1p-8f * (dc + B.R);
+                const float x = len3(cross3(w, B.A));
+                const bool line = (x - dc * B.delta - B.R) > rr + mgn;
+                const bool behind = (-dot(w, B.A) - dc * B.delta - B.R * (1.0f + B.delta)) > mgn;
+                cand = !(line || behind);  // NaN anywhere -> candidate
+            }
+        }
+    }
+    return __builtin_amdgcn_ballot_w64(cand);
+}
+
+// BUNDLE path.  Nearest hit of one segment for every active lane (converged call).  PRIMARY: TracePixel's
+// rule (:977, :987, :993) with the per-frame camera-relative constants; otherwise
+// TraceSecondaryRay's asymmetric rule (:804-806, :819-821, :825).
+
+template <bool PRIMARY>
+__device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d, bool active) {
+    const unsigned long long am = __builtin_amdgcn_ballot_w64(active);
+    if (am == 0) return Hit{0.0f, HIT_NONE};
+    const Bundle B = make_bundle(o, d, active, false);
+    if (am != ~0ull) {  // idle lanes trace an exact copy of the first active lane's ray, so
+        const int ref = __builtin_ctzll(am);  // they never add divergence (results ignored)
+        const f3 ro = readlane3(o, ref), rd = readlane3(d, ref);
+        if (!active) {
+            o = ro;
+            d = rd;
+        }
+    }
+    const float a = dot(d, d);
+    const float a2 = 2.0f * a, a4 = 4.0f * a;
+    const bool a2_ok = a2 > 0.0f && a2 < __builtin_inff();
+    float best_s = __builtin_inff();
+    int win_s = -1;
+    for (int base = 0; base < p.S; base += 64) {
+        const int n = min(64, p.S - base);
+        unsigned long long m = cull_mask(p, B, base, n);
+        while (m) {
+            const int i = base + (int)__builtin_ctzll(m);
+            m &= m - 1;
+            float t;
+            if (PRIMARY && p.prim_const) {
+                // o == camera: oc = cam - c and c = oc.oc - r^2 are per-frame constants (:614-619)
+                const PrimConst pc = p.pc[i];
+                const float b = 2.0f * dot(mk(pc.ocx, pc.ocy, pc.ocz), d);
+                const float disc = b * b - a4 * pc.c;
+                t = a2_ok ? root_t1(b, disc, a2) : root_full(b, disc, a2);
+            } else {
+                t = sphere_t(o, d, a2, a4, a2_ok, p.sph[i]);
+            }
+            if (PRIMARY) {
+                if (t > 0.0f && best_s > t) {
+                    best_s = t;
+                    win_s = i;
+                }
+            } else {
+                const float tm = t - 0.01f;
+                if (tm > 0.0f && tm < best_s) {
+                    best_s = t;
+                    win_s = i;
+                }
+            }
+        }
+    }
+    float best_p = __builtin_inff();
+    int win_p = -1;
+    for (int i = 0; i < p.P; ++i) {
+        const float t = plane_t(o, d, p.pl[i]);
+        if (t > 0.0f && t < best_p) {
+            best_p = t;
+            win_p = i;
+        }
+    }
+    if (!active) return Hit{0.0f, HIT_NONE};
+    if (best_s < best_p) return Hit{best_s, win_s};
+    if (win_p >= 0) return Hit{best_p, ~win_p};
+    return Hit{0.0f, HIT_NONE};
+}
+
+// Shading of one shaded hit per active lane (TraceSphere :847-873 / TracePlane :736-778),
+// converged call: the colour is accumulated in the reference's order -- mirror term (from
+// the deeper segment `sec`), then each light in order, then ambient.  Inactive lanes
+// return `sec` unchanged.  Shadow rays (IntersectShadowLight :573-582) of the lanes that
+// need them form one bundle per light (common direction = the light position).
+template <bool GPOW>
+__device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool is_sphere, int prim, f3 hp, f3 d, float t,
+                                    f3 sec, unsigned* n_shadow) {
+    // idle lanes (act false) carry a copy of an active lane's record: same branches, result dropped
+    const DevMaterial& m = p.mat[is_sphere ? prim : p.S + prim];
+    const uint32_t flags = m.flags;
+    f3 normal;
+    float tile = 1.0f;
+    if (is_sphere) {
+        const DevSphere& s = p.sph[prim];
+        normal = normalize(sub(hp, mk(s.cx, s.cy, s.cz)));  // SpherePhongShading :706
+    } else {
+        const DevPlane& pl = p.pl[prim];
+        normal = mk(pl.nx, pl.ny, pl.nz);
+        // checkerboard, :766-770: ((int)u + (int)v) & 1, unchecked int add
+        const float u = dot(mk(pl.e1x, pl.e1y, pl.e1z), hp);
+        const float v = dot(mk(pl.e2x, pl.e2y, pl.e2z), hp);
+        tile = (float)(int32_t)(((uint32_t)net_f2i(u) + (uint32_t)net_f2i(v)) & 1u);
+    }
+    f3 col = mk(0.0f, 0.0f, 0.0f);
+    if (flags & MAT_MIRROR) col = add(col, mul(sec, mk(m.km[0], m.km[1], m.km[2])));
+    const bool diff = act && (flags & MAT_DIFFUSE) != 0;
+    if (__builtin_amdgcn_ballot_w64(diff) != 0) {
+        const f3 view = normalize(d);  // ShapePhongShading :668 (not negated)
+        // sphere: (1 / t) * t (:866);  plane: (float)(1 / Math.Pow(t, 2)) (:754), exact as 1/(t*t) in f64
+        const float att = is_sphere ? (1.0f / t) * t : (float)(1.0 / ((double)t * (double)t));
+        const f3 kd = mk(m.kd[0], m.kd[1], m.kd[2]);
+        for (int li = 0; li < p.L; ++li) {
+            const DevLight& l = p.li[li];
+            const f3 lp = mk(l.px, l.py, l.pz);
+            const bool l_ok = l.a2 > 0.0f && l.a2 < __builtin_inff();  // wave-uniform
+            Bundle B = make_bundle(hp, lp, diff, true);
+            B.ok = B.ok && l_ok && l.a >= 0x1p-40f && l.a <= 0x1p40f;
+            const f3 hs = diff ? hp : B.O;  // idle lanes mirror a shading lane (results ignored)
+            bool blocked = !diff;
+            for (int base = 0; base < p.S; base += 64) {
+                const int n = min(64, p.S - base);
+                unsigned long long mk64 = cull_mask(p, B, base, n);
+                while (mk64) {
+                    const int i = base + (int)__builtin_ctzll(mk64);
+                    mk64 &= mk64 - 1;
+                    blocked = blocked | shadow_blocked(hs, l, l_ok, p.sph[i]);  // no short-circuit branch
+                    if (__builtin_amdgcn_ballot_w64(!blocked) == 0) break;
+                }
+                if (__builtin_amdgcn_ballot_w64(!blocked) == 0) break;
+            }
+            const float inten = (blocked || !diff) ? 0.0f : l.intensity;
+            // ShapePhongShading, :665-695
+            const f3 ldir = normalize(sub(lp, hp));
+            f3 ph = scale(kd, nmax0(dot(normal, ldir)));
+            f3 spec = mk(0.0f, 0.0f, 0.0f);
+            if (flags & MAT_SPEC) {
+                const f3 rs = sub(ldir, scale(normal, 2.0f * dot(ldir, normal)));
+                const float sp = spec_pow<GPOW>(nmax0(dot(view, normalize(rs))), m);
+                spec = mul(mk(m.ks[0], m.ks[1], m.ks[2]), mk(sp, sp, sp));
+            }
+            ph = add(ph, spec);
+            const float ia = inten * att;
+            f3 term = mul(mk(ia, ia, ia), ph);
+            if (!is_sphere) {
+                term = mul(term, mk(tile, tile, tile));
+                term = mk(nmax0(term.x), nmax0(term.y), nmax0(term.z));  // .Max(0f), :775
+            }
+            if (diff) col = add(col, term);
+        }
+        if (diff) *n_shadow += (unsigned)p.L;
+    }
+    col = add(col, mk(m.amb[0], m.amb[1], m.amb[2]));
+    return act ? col : sec;
+}
+
+// BUNDLE kernel (scenes with >= CULL_MIN_SPHERES spheres): converged control flow so that
+// every segment and every light can form a wave bundle and cull the sphere list.
+template <int K, bool SCRATCH, bool GPOW>
+__global__ __launch_bounds__(256) void trace_bundle_kernel(LaunchParams p) {
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
+    const int r = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const int band = p.band_first + (r / p.band_rows) * p.band_step;
+    const int y = band * p.band_rows + (r % p.band_rows);
+    const bool valid = x < p.W && r < p.local_rows && y < p.H;
+
+    unsigned n_prim = valid ? 1u : 0u, n_refl = 0, n_shadow = 0;
+    const f3 cam = mk(p.cam[0], p.cam[1], p.cam[2]);
+    // TracePixel primary ray, :963-971 (no half-pixel offset)
+    const float px = (float)x / (float)p.W - 0.5f;
+    const float py = (float)y / (float)p.H - 0.5f;
+    const float lx = px * p.pw, ly = py * p.ph, lz = 1.0f * p.nearc;
+    const f3 vp = add(add(add(cam, scale(mk(p.right[0], p.right[1], p.right[2]), lx)),
+                          scale(mk(p.up[0], p.up[1], p.up[2]), ly)),
+                      scale(mk(p.fwd[0], p.fwd[1], p.fwd[2]), lz));
+    f3 d = normalize(sub(vp, cam));
+    f3 o = cam;
+
+    // forward walk: all lanes advance one segment per iteration (converged loop), each
+    // shaded hit pushes a record; mirror hits continue with the reflected segment
+    LevelStack<K, SCRATCH> stk;
+    f3 leaf = mk(0.0f, 0.0f, 0.0f);
+    bool active = valid;
+    Hit h = nearest_bundle<true>(p, o, d, active);
+    for (int count = 0;; ++count) {
+        if (active) {
+            const bool is_sphere = h.prim >= 0;
+            if (h.prim == HIT_NONE || h.t - 0.01f <= 0.0f) {  // nothing hit / too close: Zero (:731, :839)
+                active = false;
+            } else if (count > p.limit) {  // terminal segment: Zero / One (:734, :843)
+                if (!is_sphere) leaf = mk(1.0f, 1.0f, 1.0f);
+                active = false;
+            } else {
+                const f3 hp = add(o, scale(d, h.t));
+                stk.push(make_float4(hp.x, hp.y, hp.z, h.t), make_float4(d.x, d.y, d.z, __int_as_float(h.prim)));
+                const int prim = is_sphere ? h.prim : ~h.prim;
+                const uint32_t flags = p.mat[is_sphere ? prim : p.S + prim].flags;
+                if (!(flags & MAT_MIRROR)) {
+                    active = false;
+                } else {
+                    f3 normal;
+                    if (is_sphere) {
+                        const DevSphere& s = p.sph[prim];
+                        normal = normalize(sub(hp, mk(s.cx, s.cy, s.cz)));  // :854
+                    } else {
+                        const DevPlane& pl = p.pl[prim];
+                        normal = mk(pl.nx, pl.ny, pl.nz);
+                    }
+                    d = sub(d, scale(normal, 2.0f * dot(d, normal)));  // CalculateReflectionRay :718-720
+                    o = hp;
+                    ++n_refl;
+                }
+            }
+        }
+        if (__builtin_amdgcn_ballot_w64(active) == 0) break;
+        h = nearest_bundle<false>(p, o, d, active);
+    }
+
+    // backward fold (converged): level by level from the deepest, every recorded hit is
+    // shaded; a mirror hit consumes the colour of the segment after it (levels 0..limit
+    // push at most one record each, so K = limit + 1 records suffice)
+    f3 col = leaf;
+    const int depth = stk.n;
+    int level = (int)wave_max((float)depth);
+    while (level-- > 0) {
+        const bool act = level < depth;  // this lane's top record is at `level`
+        float4 ra = make_float4(0.0f, 0.0f, 0.0f, 1.0f), rb = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
+        if (act) stk.pop(ra, rb);
+        const unsigned long long am = __builtin_amdgcn_ballot_w64(act);
+        if (am != ~0ull) {  // idle lanes shade a copy of the first active lane's record
+            const int ref = __builtin_ctzll(am);
+            const float4 qa = make_float4(readlane_f(ra.x, ref), readlane_f(ra.y, ref), readlane_f(ra.z, ref),
+                                          readlane_f(ra.w, ref));
+            const float4 qb = make_float4(readlane_f(rb.x, ref), readlane_f(rb.y, ref), readlane_f(rb.z, ref),
+                                          readlane_f(rb.w, ref));
+            if (!act) {
+                ra = qa;
+                rb = qb;
+            }
+        }
+        const int code = __float_as_int(rb.w);
+        const bool is_s = code >= 0;
+        col = shade_bundle<GPOW>(p, act, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z), ra.w, col,
+                          &n_shadow);
+    }
+    if (valid) {
         const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
         p.out[(size_t)r * (size_t)p.W + (size_t)x] = (int32_t)px32;
     }
@@ -431,32 +806,42 @@ __global__ __launch_bounds__(256) void scatter_bands_kernel(const int32_t* __res
     }
 }
 
-template <bool GPOW>
-static void launch_variant(const LaunchParams& p, dim3 grid, dim3 block, hipStream_t s) {
-    const int need = p.limit + 1;  // levels 0..limit can push a record
-    if (need <= 1)
-        hipLaunchKernelGGL((trace_kernel<1, false, GPOW>), grid, block, 0, s, p);
-    else if (need <= 2)
-        hipLaunchKernelGGL((trace_kernel<2, false, GPOW>), grid, block, 0, s, p);
-    else if (need <= 4)
-        hipLaunchKernelGGL((trace_kernel<4, false, GPOW>), grid, block, 0, s, p);
-    else if (need <= 6)
-        hipLaunchKernelGGL((trace_kernel<6, false, GPOW>), grid, block, 0, s, p);
-    else if (need <= 8)
-        hipLaunchKernelGGL((trace_kernel<8, false, GPOW>), grid, block, 0, s, p);
-    else
-        hipLaunchKernelGGL((trace_kernel<64, true, GPOW>), grid, block, 0, s, p);
-}
+#define RT_DEFINE_DISPATCH(NAME)                                                                 \
+    template <bool GPOW>                                                                         \
+    static void launch_##NAME(const LaunchParams& p, dim3 grid, dim3 block, hipStream_t s) {     \
+        const int need = p.limit + 1; /* levels 0..limit can push a record */                    \
+        if (need <= 1)                                                                           \
+            hipLaunchKernelGGL((NAME<1, false, GPOW>), grid, block, 0, s, p);                    \
+        else if (need <= 2)                                                                      \
+            hipLaunchKernelGGL((NAME<2, false, GPOW>), grid, block, 0, s, p);                    \
+        else if (need <= 4)                                                                      \
+            hipLaunchKernelGGL((NAME<4, false, GPOW>), grid, block, 0, s, p);                    \
+        else if (need <= 6)                                                                      \
+            hipLaunchKernelGGL((NAME<6, false, GPOW>), grid, block, 0, s, p);                    \
+        else if (need <= 8)                                                                      \
+            hipLaunchKernelGGL((NAME<8, false, GPOW>), grid, block, 0, s, p);                    \
+        else                                                                                     \
+            hipLaunchKernelGGL((NAME<64, true, GPOW>), grid, block, 0, s, p);                    \
+    }
+RT_DEFINE_DISPATCH(trace_direct_kernel)
+RT_DEFINE_DISPATCH(trace_bundle_kernel)
+#undef RT_DEFINE_DISPATCH
 
 int launch_trace(const LaunchParams& p, bool generic_pow, void* stream) {
     if (p.local_rows <= 0 || p.W <= 0) return (int)hipSuccess;
     const dim3 grid((unsigned)((p.W + 15) / 16), (unsigned)((p.local_rows + 15) / 16));
     const dim3 block(256);
     hipStream_t s = (hipStream_t)stream;
-    if (generic_pow)
-        launch_variant<true>(p, grid, block, s);
-    else
-        launch_variant<false>(p, grid, block, s);
+    // bundle culling pays for its per-wave bounds only with enough spheres (A/B: +15 % at
+    // 8 spheres, 3x faster at 64)
+    const bool bundle = p.S >= CULL_MIN_SPHERES;
+    if (generic_pow) {
+        if (bundle) launch_trace_bundle_kernel<true>(p, grid, block, s);
+        else launch_trace_direct_kernel<true>(p, grid, block, s);
+    } else {
+        if (bundle) launch_trace_bundle_kernel<false>(p, grid, block, s);
+        else launch_trace_direct_kernel<false>(p, grid, block, s);
+    }
     return (int)hipGetLastError();
 }
 

@@ -107,8 +107,9 @@ class RayTracerError(RuntimeError):
         self.code = code
 
 
-def load_library(path: str | None = None):
-    """Load libraytracer_hip.so (in-tree build).  Raises if it was not built."""
+def load_library(path: str | None = None, local: bool = False):
+    """Load libraytracer_hip.so (in-tree build).  Raises if it was not built.
+    local=True loads with RTLD_LOCAL (several builds side by side, tools/ab.py)."""
     global _lib
     if _lib is not None and path is None:
         return _lib
@@ -117,7 +118,7 @@ def load_library(path: str | None = None):
         raise RuntimeError(
             f"libraytracer_hip.so not found at {p}: run __graft_entry__.build() "
             "(there is no CPU fallback)")
-    lib = C.CDLL(p, mode=C.RTLD_GLOBAL)
+    lib = C.CDLL(p, mode=C.RTLD_LOCAL if local else C.RTLD_GLOBAL)
     for name, res, args in EXPORTS:
         fn = getattr(lib, name)
         fn.restype = res
