@@ -1,8 +1,8 @@
-"""Interleaved A/B timing of two builds of libraytracer_hip in ONE process (guide rule 24).
+"""Interleaved timing of several builds of libraytracer_hip in ONE process (guide rule 24).
 
-    python tools/ab.py LIB_A LIB_B [--config C2] [--rounds 10] [--frames 50]
+    python tools/ab.py LIB_A LIB_B [LIB_C ...] [--config C2] [--rounds 10] [--frames 50]
 
-Each round renders `frames` frames with A then B (order alternating per round); the
+Each round renders `frames` frames with every build (order rotating per round); the
 library's own HIP-event kernel times are compared (median and min per frame)."""
 import argparse
 import ctypes as C
@@ -16,7 +16,7 @@ sys.path.insert(0, os.path.join(ROOT, "uu-infogr-raytracer_amd"))
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("libs", nargs=2)
+    ap.add_argument("libs", nargs="+")
     ap.add_argument("--config", default="C2")
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--frames", type=int, default=50)
@@ -38,11 +38,12 @@ def main():
         assert lib.rt_set_camera(ctx, C.byref(sc.c_camera())) == 0
         libs.append(lib)
         ctxs.append(ctx)
-    frames = {0: [], 1: []}
+    nl = len(libs)
+    frames = {i: [] for i in range(nl)}
     crcs = {}
     import zlib
     for rnd in range(a.rounds + 1):
-        order = (0, 1) if rnd % 2 == 0 else (1, 0)
+        order = [(rnd + j) % nl for j in range(nl)]
         for i in order:
             lib, ctx = libs[i], ctxs[i]
             lib.rt_reset_stats(ctx)
@@ -53,11 +54,12 @@ def main():
             if rnd > 0:  # round 0 = warm-up
                 frames[i].append(st.kernel_ms / st.launches)
             crcs[i] = zlib.crc32(out.cpu().numpy().tobytes())
-    for i in (0, 1):
+    for i in range(nl):
         v = frames[i]
         print(f"{os.path.basename(a.libs[i]):32s} {a.config}: median {statistics.median(v)*1e3:8.2f} us  "
               f"min {min(v)*1e3:8.2f} us  crc {crcs[i]:08x}")
-    print(f"B/A median ratio {statistics.median(frames[1]) / statistics.median(frames[0]):.3f}")
+    for i in range(1, nl):
+        print(f"{os.path.basename(a.libs[i])}/A median ratio {statistics.median(frames[i]) / statistics.median(frames[0]):.3f}")
 
 
 if __name__ == "__main__":

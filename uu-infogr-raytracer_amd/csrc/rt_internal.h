@@ -67,6 +67,7 @@ constexpr int MAX_PRIM_CONST = 64;
 // Scenes with at least this many spheres use wave-bundle culling (rt_kernel.hip).
 constexpr int CULL_MIN_SPHERES = 12;
 
+
 // Per-launch parameters (passed by value as the kernel argument block, < 4 KiB).
 struct LaunchParams {
     const DevSphere* sph;

@@ -24,6 +24,12 @@
 
 #include "rt_internal.h"
 
+// RT_ABLATE (timing experiments only, tools/ab.py; never defined in the shipped build):
+//   1 = no shading (fold skipped), 2 = no shadow rays, 3 = primary segment only.
+#ifndef RT_ABLATE
+#define RT_ABLATE 0
+#endif
+
 namespace rtk {
 
 struct f3 {
@@ -210,6 +216,21 @@ __device__ __forceinline__ unsigned wave_sum(unsigned v) {
     return v;
 }
 
+// Sphere loop of the direct path: a runtime loop (SMAX = 0, shipped) or fully unrolled over
+// SMAX with uniform `i < S` guards.  In-process A/B of SMAX = 8: C2 +2.7 %, C3 -3.3 % -- not
+// taken.
+template <int SMAX, typename F>
+__device__ __forceinline__ void for_spheres(int S, F&& f) {
+    if constexpr (SMAX > 0) {
+#pragma unroll
+        for (int i = 0; i < SMAX; ++i)
+            if (i < S) f(i);
+    } else {
+#pragma unroll 2
+        for (int i = 0; i < S; ++i) f(i);
+    }
+}
+
 // Result of a nearest-hit search.
 struct Hit {
     float t;
@@ -221,7 +242,7 @@ constexpr int HIT_NONE = 0x7fffffff;
 // Shading of one shaded hit (TraceSphere :847-873 / TracePlane :736-778): the colour is
 // accumulated in the reference's order -- mirror term (from the deeper segment `sec`),
 // then each light, then ambient.  Returns the colour; adds shadow rays to *n_shadow.
-template <bool GPOW>
+template <bool GPOW, int SMAX>
 __device__ __forceinline__ f3 shade_direct(const LaunchParams& p, bool is_sphere, int prim, f3 hp, f3 d, float t, f3 sec,
                                     unsigned* n_shadow) {
     const DevMaterial& m = p.mat[is_sphere ? prim : p.S + prim];
@@ -250,7 +271,15 @@ __device__ __forceinline__ f3 shade_direct(const LaunchParams& p, bool is_sphere
             const DevLight& l = p.li[li];
             const bool l_ok = l.a2 > 0.0f && l.a2 < __builtin_inff();  // wave-uniform
             bool blocked = false;
-            for (int i = 0; i < p.S && !blocked; ++i) blocked = shadow_blocked(hp, l, l_ok, p.sph[i]);
+            if constexpr (RT_ABLATE == 2) {
+                blocked = hp.x > 1e30f;
+            } else if constexpr (SMAX > 0) {
+                for_spheres<SMAX>(p.S, [&](int i) {
+                    if (!blocked) blocked = shadow_blocked(hp, l, l_ok, p.sph[i]);
+                });
+            } else {
+                for (int i = 0; i < p.S && !blocked; ++i) blocked = shadow_blocked(hp, l, l_ok, p.sph[i]);
+            }
             const float inten = blocked ? 0.0f : l.intensity;
             // ShapePhongShading, :665-695
             const f3 ldir = normalize(sub(mk(l.px, l.py, l.pz), hp));
@@ -275,7 +304,7 @@ __device__ __forceinline__ f3 shade_direct(const LaunchParams& p, bool is_sphere
     return add(col, mk(m.amb[0], m.amb[1], m.amb[2]));
 }
 
-template <bool PRIMARY>
+template <bool PRIMARY, int SMAX>
 __device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d) {
     const float a = dot(d, d);
     const float a2 = 2.0f * a, a4 = 4.0f * a;
@@ -284,8 +313,7 @@ __device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d)
     int win_s = -1;
     if (PRIMARY && p.prim_const) {
         // o == camera: oc = cam - c and c = oc.oc - r^2 are the same per frame (:614-619)
-#pragma unroll 2
-        for (int i = 0; i < p.S; ++i) {
+        for_spheres<SMAX>(p.S, [&](int i) {
             const PrimConst pc = p.pc[i];
             const float b = 2.0f * dot(mk(pc.ocx, pc.ocy, pc.ocz), d);
             const float disc = b * b - a4 * pc.c;
@@ -294,10 +322,9 @@ __device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d)
                 best_s = t;
                 win_s = i;
             }
-        }
+        });
     } else {
-#pragma unroll 2
-        for (int i = 0; i < p.S; ++i) {
+        for_spheres<SMAX>(p.S, [&](int i) {
             const float t = sphere_t(o, d, a2, a4, a2_ok, p.sph[i]);
             if (PRIMARY) {
                 if (t > 0.0f && best_s > t) {
@@ -311,7 +338,7 @@ __device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d)
                     win_s = i;
                 }
             }
-        }
+        });
     }
     float best_p = __builtin_inff();
     int win_p = -1;
@@ -328,7 +355,7 @@ __device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d)
 }
 
 // DIRECT kernel: each lane walks its own chain with per-lane (divergent) control flow.
-template <int K, bool SCRATCH, bool GPOW>
+template <int K, bool SCRATCH, bool GPOW, int SMAX>
 __global__ __launch_bounds__(256) void trace_direct_kernel(LaunchParams p) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
@@ -354,7 +381,7 @@ __global__ __launch_bounds__(256) void trace_direct_kernel(LaunchParams p) {
 
         LevelStack<K, SCRATCH> stk;
         f3 leaf = mk(0.0f, 0.0f, 0.0f);
-        Hit h = nearest_direct<true>(p, o, d);
+        Hit h = nearest_direct<true, SMAX>(p, o, d);
         int count = 0;
         for (;;) {
             if (h.prim == HIT_NONE) break;      // nothing hit: plane colour stays Zero
@@ -369,7 +396,7 @@ __global__ __launch_bounds__(256) void trace_direct_kernel(LaunchParams p) {
             stk.push(make_float4(hp.x, hp.y, hp.z, h.t), make_float4(d.x, d.y, d.z, __int_as_float(h.prim)));
             const int prim = is_sphere ? h.prim : ~h.prim;
             const uint32_t flags = p.mat[is_sphere ? prim : p.S + prim].flags;
-            if (!(flags & MAT_MIRROR)) break;
+            if (!(flags & MAT_MIRROR) || RT_ABLATE == 3) break;
             f3 normal;
             if (is_sphere) {
                 const DevSphere& s = p.sph[prim];
@@ -382,18 +409,25 @@ __global__ __launch_bounds__(256) void trace_direct_kernel(LaunchParams p) {
             o = hp;
             ++count;
             ++n_refl;
-            h = nearest_direct<false>(p, o, d);
+            h = nearest_direct<false, SMAX>(p, o, d);
         }
         // backward fold: every recorded hit is shaded in reverse order; a mirror hit
         // consumes the colour of the segment after it (levels 0..limit push at most one
         // record each, so K = limit + 1 records suffice)
         f3 col = leaf;
-        while (stk.n > 0) {
+        if constexpr (RT_ABLATE == 1) {  // keep the walk alive: fold the records' t into the colour
+            while (stk.n > 0) {
+                float4 ra, rb;
+                stk.pop(ra, rb);
+                col.x += ra.w;
+            }
+        }
+        while (RT_ABLATE != 1 && stk.n > 0) {
             float4 ra, rb;
             stk.pop(ra, rb);
             const int code = __float_as_int(rb.w);
             const bool is_s = code >= 0;
-            col = shade_direct<GPOW>(p, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z), ra.w, col,
+            col = shade_direct<GPOW, SMAX>(p, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z), ra.w, col,
                               &n_shadow);
         }
         const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
@@ -806,25 +840,25 @@ __global__ __launch_bounds__(256) void scatter_bands_kernel(const int32_t* __res
     }
 }
 
-#define RT_DEFINE_DISPATCH(NAME)                                                                 \
+#define RT_DEFINE_DISPATCH(FN, NAME, ...)                                                        \
     template <bool GPOW>                                                                         \
-    static void launch_##NAME(const LaunchParams& p, dim3 grid, dim3 block, hipStream_t s) {     \
+    static void FN(const LaunchParams& p, dim3 grid, dim3 block, hipStream_t s) {                \
         const int need = p.limit + 1; /* levels 0..limit can push a record */                    \
         if (need <= 1)                                                                           \
-            hipLaunchKernelGGL((NAME<1, false, GPOW>), grid, block, 0, s, p);                    \
+            hipLaunchKernelGGL((NAME<1, false, GPOW __VA_ARGS__>), grid, block, 0, s, p);        \
         else if (need <= 2)                                                                      \
-            hipLaunchKernelGGL((NAME<2, false, GPOW>), grid, block, 0, s, p);                    \
+            hipLaunchKernelGGL((NAME<2, false, GPOW __VA_ARGS__>), grid, block, 0, s, p);        \
         else if (need <= 4)                                                                      \
-            hipLaunchKernelGGL((NAME<4, false, GPOW>), grid, block, 0, s, p);                    \
+            hipLaunchKernelGGL((NAME<4, false, GPOW __VA_ARGS__>), grid, block, 0, s, p);        \
         else if (need <= 6)                                                                      \
-            hipLaunchKernelGGL((NAME<6, false, GPOW>), grid, block, 0, s, p);                    \
+            hipLaunchKernelGGL((NAME<6, false, GPOW __VA_ARGS__>), grid, block, 0, s, p);        \
         else if (need <= 8)                                                                      \
-            hipLaunchKernelGGL((NAME<8, false, GPOW>), grid, block, 0, s, p);                    \
+            hipLaunchKernelGGL((NAME<8, false, GPOW __VA_ARGS__>), grid, block, 0, s, p);        \
         else                                                                                     \
-            hipLaunchKernelGGL((NAME<64, true, GPOW>), grid, block, 0, s, p);                    \
+            hipLaunchKernelGGL((NAME<64, true, GPOW __VA_ARGS__>), grid, block, 0, s, p);        \
     }
-RT_DEFINE_DISPATCH(trace_direct_kernel)
-RT_DEFINE_DISPATCH(trace_bundle_kernel)
+RT_DEFINE_DISPATCH(launch_direct_loop, trace_direct_kernel, , 0)
+RT_DEFINE_DISPATCH(launch_bundle, trace_bundle_kernel)
 #undef RT_DEFINE_DISPATCH
 
 int launch_trace(const LaunchParams& p, bool generic_pow, void* stream) {
@@ -836,11 +870,11 @@ int launch_trace(const LaunchParams& p, bool generic_pow, void* stream) {
     // 8 spheres, 3x faster at 64)
     const bool bundle = p.S >= CULL_MIN_SPHERES;
     if (generic_pow) {
-        if (bundle) launch_trace_bundle_kernel<true>(p, grid, block, s);
-        else launch_trace_direct_kernel<true>(p, grid, block, s);
+        if (bundle) launch_bundle<true>(p, grid, block, s);
+        else launch_direct_loop<true>(p, grid, block, s);
     } else {
-        if (bundle) launch_trace_bundle_kernel<false>(p, grid, block, s);
-        else launch_trace_direct_kernel<false>(p, grid, block, s);
+        if (bundle) launch_bundle<false>(p, grid, block, s);
+        else launch_direct_loop<false>(p, grid, block, s);
     }
     return (int)hipGetLastError();
 }
