@@ -38,6 +38,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="C2")
     ap.add_argument("--band-rows", type=int, default=8)
+    ap.add_argument("--no-pipeline", action="store_true",
+                    help="N>1: gather each frame before tracing the next (no double buffering)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -117,6 +119,9 @@ def main():
     stream = torch.cuda.current_stream()
     s = stream.cuda_stream
 
+    def finish():
+        pass
+
     if world == 1:
         frame = torch.empty(W * H, dtype=torch.int32, device="cuda")
         px_per_launch = W * H
@@ -124,22 +129,37 @@ def main():
         def step():
             ctx.render_device(W, H, frame.data_ptr(), s)
     else:
-        from raytracer_hip.dist import BandGather, RowBands
+        from raytracer_hip.dist import BandGather, PipelinedBandGather, RowBands
         rb = RowBands(W, H, args.band_rows, rank, world)
-        bg = BandGather(rb, torch.device("cuda", local))
         px_per_launch = rb.pixels
         frame = torch.empty(W * H, dtype=torch.int32, device="cuda") if rank == 0 else None
 
-        def step():
-            # trace this rank's bands -> RCCL gather of the slots to rank 0 -> reassemble there
-            ctx.render_bands(W, H, rb.band_rows, rank, world, bg.local.data_ptr(), s)
-            parts = bg.gather()
-            if rank == 0:
+        def scatter(parts):
+            if rank == 0 and parts is not None:
                 for r in range(world):
                     ctx.scatter_bands(W, H, rb.band_rows, r, world, parts[r].data_ptr(), frame.data_ptr(), s)
 
+        if args.no_pipeline:
+            bg = BandGather(rb, torch.device("cuda", local))
+
+            def step():
+                # trace this rank's bands -> RCCL gather of the slots to rank 0 -> reassemble there
+                ctx.render_bands(W, H, rb.band_rows, rank, world, bg.local.data_ptr(), s)
+                scatter(bg.gather())
+        else:
+            pg = PipelinedBandGather(rb, torch.device("cuda", local))
+
+            def step():
+                # trace frame k into one slot while frame k-1's RCCL gather is in flight
+                ctx.render_bands(W, H, rb.band_rows, rank, world, pg.buffer().data_ptr(), s)
+                scatter(pg.submit())
+
+            def finish():  # noqa: F811  -- the last frame's gather and reassembly
+                scatter(pg.drain())
+
     for _ in range(args.warmup):
         step()
+    finish()
     torch.cuda.synchronize()
     ctx.reset_stats()
 
@@ -149,6 +169,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    finish()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
@@ -191,7 +212,8 @@ def main():
                 "width": W, "height": H, "spheres": len(sc.spheres), "planes": len(sc.planes),
                 "lights": len(sc.lights), "depth": sc.recursion_limit + 1,
                 "parallelism": "single GPU" if world == 1 else
-                f"interleaved {args.band_rows}-row bands x {world} ranks + RCCL gather to rank 0",
+                f"interleaved {args.band_rows}-row bands x {world} ranks + RCCL gather to rank 0"
+                + ("" if args.no_pipeline else " (double-buffered: gather k overlaps trace k+1)"),
                 "rays_per_frame": rays_per_frame,
             },
             "roofline": {

@@ -44,3 +44,54 @@ def run(rank, world, port, cfg, width, height, band_rows, result_path):
         assert ok.item() == 1
     finally:
         dist.destroy_process_group()
+
+
+def run_pipelined(rank, world, port, cfg, width, height, band_rows, frames, result_path):
+    """Consecutive frames (a different camera yaw each) through PipelinedBandGather; rank 0
+    checks every reassembled frame against the oracle's full frame for that camera."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path[:0] = [os.path.join(root, "uu-infogr-raytracer_amd"), os.path.join(root, "oracle"), here]
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import pyoracle
+    from raytracer_hip import scenes
+    from raytracer_hip.dist import PipelinedBandGather, RowBands, scatter_host
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        base = scenes.config(cfg).resized(width, height)
+
+        def scene_for(k):
+            sc = base.resized(width, height)
+            sc.camera = ((0.0, 0.0, 0.0), 0.05 * k - 0.1, 0.02 * k)
+            return sc
+
+        rb = RowBands(width, height, band_rows, rank, world)
+        pg = PipelinedBandGather(rb, "cpu")
+        got = []
+        for k in range(frames):
+            local = pg.buffer().numpy().reshape(-1, width)
+            local[:] = -3
+            for l0, y0, n in rb.row_spans():
+                rows, _ = pyoracle.render(scene_for(k), pyoracle.MODE_NEAREST, 2, rows=(y0, y0 + n))
+                local[l0:l0 + n] = rows
+            done = pg.submit()
+            if done is not None and rank == 0:
+                got.append(scatter_host([t.numpy() for t in done], width, height, band_rows))
+        done = pg.drain()
+        if rank == 0:
+            got.append(scatter_host([t.numpy() for t in done], width, height, band_rows))
+            bad = []
+            for k, frame in enumerate(got):
+                full, _ = pyoracle.render(scene_for(k), pyoracle.MODE_NEAREST, 2)
+                if not np.array_equal(frame, full):
+                    bad.append(k)
+            with open(result_path, "w") as f:
+                f.write("ok" if len(got) == frames and not bad else f"bad frames {bad} of {len(got)}")
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()

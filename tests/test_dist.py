@@ -64,3 +64,24 @@ def test_gloo_band_gather_reassembles_oracle_frame(tmp_path, world, cfg, w, h, b
             p.kill()
     assert codes == [0] * world, codes
     assert result.read_text() == "ok"
+
+
+@pytest.mark.parametrize("world,frames", [(2, 5), (3, 4)])
+def test_gloo_pipelined_gather_keeps_frames_apart(tmp_path, world, frames):
+    """Double-buffered gather (bench.py's N>1 step): every frame reassembles to its own oracle frame."""
+    import dist_worker
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    result = tmp_path / "result.txt"
+    procs = [ctx.Process(target=dist_worker.run_pipelined,
+                         args=(r, world, port, "C3", 48, 35, 4, frames, str(result))) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0] * world, codes
+    assert result.read_text() == "ok"

@@ -75,3 +75,54 @@ class BandGather:
         import torch.distributed as dist
         dist.gather(self.local, self.parts, dst=0)
         return self.parts
+
+
+class PipelinedBandGather:
+    """Double-buffered gather: frame k's gather overlaps frame k+1's trace.
+
+    Per frame:  buf = pg.buffer()  -> trace this rank's bands into `buf`
+                done = pg.submit() -> starts the gather of `buf` (async), then waits for
+                                      the previous frame's gather and returns its slots
+                                      (rank 0; None elsewhere / on the first frame)
+    and finally `pg.drain()` returns the last frame's slots.
+
+    Ordering on GPUs (ProcessGroupNCCL): the collective waits for the current stream's work
+    enqueued before it (the trace of its buffer); `wait()` makes the current stream wait for
+    the collective.  The wait for gather k is issued after trace k+1 was enqueued (overlap)
+    and before trace k+2 reuses gather k's buffer, and rank 0 consumes gather k's slots
+    after that wait; gather k+2 into the same slots is ordered after that consumption.
+    """
+
+    def __init__(self, rb: RowBands, device, depth: int = 2):
+        import torch
+        self.rb = rb
+        self.depth = depth
+        self.local = [torch.zeros(rb.slot_elems, dtype=torch.int32, device=device) for _ in range(depth)]
+        self.parts = [[torch.empty_like(self.local[0]) for _ in range(rb.world)] if rb.rank == 0 else None
+                      for _ in range(depth)]
+        self.frame = 0
+        self.pending = None  # (work, slot index)
+
+    def buffer(self):
+        return self.local[self.frame % self.depth]
+
+    def submit(self):
+        import torch.distributed as dist
+        i = self.frame % self.depth
+        work = dist.gather(self.local[i], self.parts[i], dst=0, async_op=True)
+        done = None
+        if self.pending is not None:
+            pw, pi = self.pending
+            pw.wait()
+            done = self.parts[pi]
+        self.pending = (work, i)
+        self.frame += 1
+        return done
+
+    def drain(self):
+        if self.pending is None:
+            return None
+        pw, pi = self.pending
+        pw.wait()
+        self.pending = None
+        return self.parts[pi]
