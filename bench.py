@@ -223,7 +223,7 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS,
                 "traffic": traffic,
-                "kernel": "trace_kernel",
+                "kernel": "trace_direct_kernel" if sc and len(sc.spheres) < 12 else "trace_bundle_kernel",
                 "kernel_avg_ms": kernel_s * 1e3,
                 "note": "algorithmic bytes = 4 B framebuffer store per pixel; the path is FP32-VALU-bound",
             },

@@ -13,7 +13,7 @@ import sys
 from collections import defaultdict
 
 
-def summarise(d, kernel="trace_kernel"):
+def summarise(d, kernel="rtk::trace_"):
     vals = defaultdict(lambda: defaultdict(float))  # counter -> dispatch -> value
     for fn in sorted(glob.glob(os.path.join(d, "p*", "*counter_collection.csv"))):
         for row in csv.DictReader(open(fn)):
@@ -26,7 +26,7 @@ def summarise(d, kernel="trace_kernel"):
 
 def main():
     d = sys.argv[1]
-    kernel = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].startswith("--") else "trace_kernel"
+    kernel = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].startswith("--") else "rtk::trace_"
     s = summarise(d, kernel)
     for k in sorted(s):
         print(f"{k:32s} {s[k]:,.1f}")
