@@ -210,6 +210,71 @@ struct LevelStack<K, true> {
     }
 };
 
+// Hybrid stack for limits 3..7: the two most recent records in VGPRs, older ones in a
+// per-lane scratch array (touched only by lanes more than two levels deep -- rare), so the
+// kernel keeps its occupancy: 16 VGPRs instead of 8 x K.
+template <int K>
+struct HybridOverflow {
+    float4 a[K - 2], b[K - 2];  // older records (dynamically indexed: scratch)
+};
+template <int K>
+struct HybridStack {
+    float4 a0, b0, a1, b1;  // top record, second record (separate SSA values: VGPRs)
+    HybridOverflow<K>* ov;  // a separate object, so only it is demoted to scratch
+    int n = 0;
+    __device__ __forceinline__ explicit HybridStack(HybridOverflow<K>* o) : ov(o) {}
+    __device__ __forceinline__ void push(float4 x, float4 y) {
+        if (n >= 2) {  // spill the second record
+            ov->a[n - 2] = a1;
+            ov->b[n - 2] = b1;
+        }
+        a1 = a0;
+        b1 = b0;
+        a0 = x;
+        b0 = y;
+        ++n;
+    }
+    __device__ __forceinline__ void pop(float4& x, float4& y) {
+        x = a0;
+        y = b0;
+        a0 = a1;
+        b0 = b1;
+        --n;
+        if (n >= 2) {  // refill the second record
+            a1 = ov->a[n - 2];
+            b1 = ov->b[n - 2];
+        }
+    }
+};
+
+struct NoOverflow {};
+template <int K, bool SCRATCH>
+struct PlainStack : LevelStack<K, SCRATCH> {
+    __device__ __forceinline__ explicit PlainStack(NoOverflow*) {}
+};
+
+// Stack type per K: registers up to 2 records, hybrid up to 8, scratch beyond.
+template <int K, bool SCRATCH>
+struct StackFor {
+    using type = PlainStack<K, SCRATCH>;
+    using overflow = NoOverflow;
+};
+template <>
+struct StackFor<4, false> {
+    using type = HybridStack<4>;
+    using overflow = HybridOverflow<4>;
+};
+template <>
+struct StackFor<6, false> {
+    using type = HybridStack<6>;
+    using overflow = HybridOverflow<6>;
+};
+template <>
+struct StackFor<8, false> {
+    using type = HybridStack<8>;
+    using overflow = HybridOverflow<8>;
+};
+
 __device__ __forceinline__ unsigned wave_sum(unsigned v) {
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -379,7 +444,8 @@ __global__ __launch_bounds__(256) void trace_direct_kernel(LaunchParams p) {
         f3 d = normalize(sub(vp, cam));
         f3 o = cam;
 
-        LevelStack<K, SCRATCH> stk;
+        typename StackFor<K, SCRATCH>::overflow ovf;
+        typename StackFor<K, SCRATCH>::type stk(&ovf);
         f3 leaf = mk(0.0f, 0.0f, 0.0f);
         Hit h = nearest_direct<true, SMAX>(p, o, d);
         int count = 0;
@@ -739,7 +805,8 @@ __global__ __launch_bounds__(256) void trace_bundle_kernel(LaunchParams p) {
 
     // forward walk: all lanes advance one segment per iteration (converged loop), each
     // shaded hit pushes a record; mirror hits continue with the reflected segment
-    LevelStack<K, SCRATCH> stk;
+    typename StackFor<K, SCRATCH>::overflow ovf;
+    typename StackFor<K, SCRATCH>::type stk(&ovf);
     f3 leaf = mk(0.0f, 0.0f, 0.0f);
     bool active = valid;
     Hit h = nearest_bundle<true>(p, o, d, active);
