@@ -95,7 +95,8 @@ __device__ __forceinline__ float root_t1(float b, float disc, float a2) {
     if (disc >= 0.0f && b < 0.0f) {
         const float sq = __builtin_sqrtf(disc);  // == (float)Math.Sqrt((double)disc)
         const float nb = -b;
-        if (nb > sq) t = (nb - sq) / a2;
+        const float q = (nb - sq) / a2;  // predicated, not branched: one exec-mask region less
+        t = nb > sq ? q : 0.0f;
     }
     return t;
 }
@@ -130,12 +131,13 @@ __device__ __forceinline__ bool shadow_blocked(f3 hp, const DevLight& l, bool a2
     const float c = dot(oc, oc) - s.r2;
     const float disc = b * b - l.a4 * c;
     if (a2_ok) {
+        bool hit = false;
         if (disc >= 0.0f && b < 0.0f) {
             const float sq = __builtin_sqrtf(disc);
             const float nb = -b;
-            if (nb > sq) return (nb - sq) / l.a2 - 0.001f > 0.0f;
+            hit = (nb > sq) & ((nb - sq) / l.a2 - 0.001f > 0.0f);
         }
-        return false;
+        return hit;
     }
     if (disc >= 0.0f) {
         const float sq = __builtin_sqrtf(disc);
