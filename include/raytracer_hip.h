@@ -191,6 +191,39 @@ int rt_render_bands(rt_ctx* ctx, int width, int height, int band_rows, int band_
 int rt_scatter_bands(rt_ctx* ctx, int width, int height, int band_rows, int band_first,
                      int band_step, const int32_t* d_bands, int32_t* d_frame, void* hip_stream);
 
+/* ---- double-buffered frames ------------------------------ */
+/* Asynchronous Tick(): captures the current camera, enqueues the trace and the D2H copy
+ * into the caller's host buffer pixels[width*height] and returns at once.  rt_wait blocks
+ * until every enqueued frame is complete.  With two host buffers a caller overlaps the
+ * trace of frame k+1 with its own use of frame k (the camera of k+1 can already be set).
+ * The context keeps two device frame buffers; frames complete in enqueue order.
+ * Multi-GPU contexts render synchronously here (rt_render). */
+int rt_render_async(rt_ctx* ctx, int width, int height, int32_t* pixels);
+int rt_wait(rt_ctx* ctx);
+
+/* ---- headless display hand-off --------------------------- */
+/* Writes pixels (0x00RRGGBB, row-major) as a binary PPM (P6).  Host only, no context. */
+int rt_write_ppm(const char* path, const int32_t* pixels, int width, int height);
+
+/* ---- debug ray view (RayTracer.cs:423-435, :903-934) ------- */
+/* The reference's DEBUG_ENABLE view logs traced rays and draws 500 random ones as lines
+ * (red primary, green secondary, blue shadow) into the lower-right 30 % inset.  Here the
+ * pixels y*width+x with (y*width+x) % sample_stride == 0 are traced again and every segment
+ * of their visible path is appended to out[] (at most `capacity`; *out_count receives the
+ * total): primary/secondary segments end at the winning hit point (origin + 100*dir when
+ * nothing is hit); shadow segments start at the shaded point with the light POSITION as
+ * direction (Q2) and end at the first blocker's distance, or at t = 1 when unblocked.
+ * Synchronous.  Composited on the host by raytracer_hip.debugview. */
+typedef struct rt_segment {
+    rt_vec3 origin;
+    rt_vec3 end;
+    int32_t kind;   /* 0 primary, 1 secondary (reflected), 2 shadow -- RayKind, :343-361 */
+    int32_t pixel;  /* y*width + x */
+} rt_segment;
+
+int rt_debug_segments(rt_ctx* ctx, int width, int height, int sample_stride, rt_segment* out,
+                      int capacity, int* out_count);
+
 /* ---- statistics ------------------------------------------------------------- */
 /* Synchronises the context's pending work, then returns the counters. */
 int rt_get_stats(rt_ctx* ctx, rt_stats* out_stats);

@@ -154,3 +154,20 @@ def test_reference_scene_verbatim():
     assert mirror.material.km == (1.0, 1.0, 1.0) and mirror.material.kd == (0, 0, 0)
     pl = sc.planes[0]
     assert pl.material.n == 0.5 and pl.material.km == (1.0, 1.0, 1.0) and pl.material.ka == (0.5, 0.5, 0.5)
+
+
+def test_write_ppm_roundtrip(tmp_path):
+    """Headless display hand-off (rt_write_ppm): P6 header and RGB bytes from 0x00RRGGBB."""
+    from raytracer_hip import Surface
+    s = Surface(5, 3)
+    s.pixels[:] = np.arange(15, dtype=np.int32) * 0x010203 + 0x00102030
+    path = str(tmp_path / "f.ppm")
+    s.save_ppm(path)
+    data = open(path, "rb").read()
+    head = b"P6\n5 3\n255\n"
+    assert data.startswith(head)
+    rgb = np.frombuffer(data[len(head):], dtype=np.uint8).reshape(15, 3)
+    u = s.pixels.view(np.uint32)
+    assert (rgb[:, 0] == (u >> 16) & 255).all() and (rgb[:, 1] == (u >> 8) & 255).all() and (rgb[:, 2] == u & 255).all()
+    lib = abi.load_library()
+    assert lib.rt_write_ppm(None, None, 1, 1) == abi.RT_ERR_INVALID_ARG

@@ -211,3 +211,93 @@ def test_stats_accumulate_and_reset(gpu_ctx, golden):
     assert st["kernel_ms"] > 0 and st["copy_ms"] > 0
     gpu_ctx.reset_stats()
     assert gpu_ctx.stats()["primary_rays"] == 0
+
+
+def test_render_async_double_buffered_frames(oracle):
+    """rt_render_async into two alternating host buffers with a new camera per frame
+    (SURVEY 8f rank 1): every frame equals the oracle's frame for its own camera."""
+    sc = scenes.reference(96, 72)
+    W, H = sc.width, sc.height
+    bufs = [np.zeros(W * H, dtype=np.int32) for _ in range(2)]
+    cams = [((0.1 * k, 0.0, -0.2 * k), 0.07 * k, -0.03 * k) for k in range(6)]
+    with Context(1) as ctx:
+        ctx.set_scene(sc)
+        for b in bufs:
+            ctx.register_host(b)
+        got = []
+        for k, (pos, yaw, pitch) in enumerate(cams):
+            ctx.set_camera(abi.rt_camera(abi.rt_vec3(*pos), yaw, pitch))
+            ctx.render_async(W, H, bufs[k % 2])
+            if k >= 1:  # frame k-1 is read while frame k traces (wait covers both: in-order stream)
+                ctx.wait()
+                got.append(bufs[(k - 1) % 2].reshape(H, W).copy())
+        ctx.wait()
+        got.append(bufs[(len(cams) - 1) % 2].reshape(H, W).copy())
+        for b in bufs:
+            ctx.unregister_host(b)
+    for k, (pos, yaw, pitch) in enumerate(cams):
+        s2 = scenes.reference(W, H)
+        s2.camera = (pos, float(np.float32(yaw)), float(np.float32(pitch)))
+        want, _ = oracle.render(s2, oracle.MODE_NEAREST, 4)
+        assert_same(got[k], want, f"async frame {k}")
+
+
+@pytest.mark.parametrize("cid,w,h", [("REF", 96, 64), ("C3", 80, 45), ("C4", 64, 36)])
+def test_debug_segments_match_visible_path_ray_counts(gpu_ctx, oracle, cid, w, h):
+    """rt_debug_segments with stride 1: one segment per visible-path ray,
+    so the per-kind counts equal the oracle's primary / reflect / shadow ray counts."""
+    sc = scenes.config(cid).resized(w, h)
+    gpu_ctx.set_scene(sc)
+    segs, total = gpu_ctx.debug_segments(w, h, sample_stride=1, capacity=w * h * 64)
+    _, st = oracle.render(sc, oracle.MODE_NEAREST, 4)
+    assert total == len(segs)
+    kinds = np.bincount(segs["kind"], minlength=3)
+    assert kinds.tolist() == [st["primary_rays"], st["reflect_rays"], st["shadow_rays"]]
+    assert (segs["pixel"] >= 0).all() and (segs["pixel"] < w * h).all()
+    prim = segs[segs["kind"] == 0]
+    assert np.array_equal(np.sort(prim["pixel"]), np.arange(w * h))
+    cam = np.array(sc.camera[0], dtype=np.float32)
+    assert (prim["ox"] == cam[0]).all() and (prim["oy"] == cam[1]).all() and (prim["oz"] == cam[2]).all()
+    for f in ("ox", "oy", "oz", "ex", "ey", "ez"):
+        assert np.isfinite(segs[f]).all()
+
+
+def test_debug_segments_stride_and_capacity(gpu_ctx):
+    sc = scenes.reference(100, 60)
+    gpu_ctx.set_scene(sc)
+    segs, total = gpu_ctx.debug_segments(100, 60, sample_stride=7, capacity=100 * 60)
+    prim = segs[segs["kind"] == 0]
+    assert len(prim) == -(-6000 // 7) and (prim["pixel"] % 7 == 0).all()
+    small, total2 = gpu_ctx.debug_segments(100, 60, sample_stride=7, capacity=10)
+    assert total2 == total and len(small) == 10  # a full buffer keeps the count of every append
+    import ctypes as C
+    n = C.c_int(0)
+    lib = gpu_ctx.lib
+    assert lib.rt_debug_segments(gpu_ctx.ptr, 100, 60, 0, None, 0, C.byref(n)) == abi.RT_ERR_INVALID_ARG
+    assert lib.rt_debug_segments(gpu_ctx.ptr, 100, 60, 1, None, 5, C.byref(n)) == abi.RT_ERR_INVALID_ARG
+    assert lib.rt_debug_segments(gpu_ctx.ptr, 100, 60, 1, None, 0, C.byref(n)) == abi.RT_OK and n.value > 6000
+
+
+def test_debug_tick_composites_inset_over_exact_frame(oracle):
+    """RayTracer(debug=True).Tick(): the DEBUG_ENABLE frame -- outside the inset every pixel
+    is the traced pixel or a white circle point; inside only inset colours."""
+    from raytracer_hip import DebugView, debugview
+    screen = Surface(160, 120)
+    rt = RayTracer(screen, debug=True)
+    try:
+        rt.Tick()
+    finally:
+        rt.close()
+    want, _ = oracle.render(scenes.reference(160, 120), oracle.MODE_NEAREST, 4)
+    img = screen.image()
+    v = DebugView(160, 120)
+    inset = v.inset_mask()  # black: x > TopLeftX && y > TopLeftY
+    lines = np.zeros_like(inset)  # ClampToDebugView is inclusive of TopLeft
+    lines[v.top_left_y:, v.top_left_x:] = True
+    diff = ~lines & (img != want)
+    assert (img[diff] == debugview.CIRCLE_COLOR).all()
+    edge = lines & ~inset & (img != want)
+    assert set(np.unique(img[edge]).tolist()) <= {debugview.CIRCLE_COLOR, *debugview.KIND_COLORS.values()}
+    colours = set(np.unique(img[inset]).tolist())
+    assert colours <= {0, debugview.CIRCLE_COLOR, *debugview.KIND_COLORS.values()}
+    assert colours & set(debugview.KIND_COLORS.values())

@@ -79,6 +79,9 @@ struct Device {
     size_t bands_cap = 0;
     int32_t* d_gather = nullptr;  // device 0: n_gpus x padded band sets
     size_t gather_cap = 0;
+    int32_t* d_frames2[2] = {nullptr, nullptr};  // rt_render_async double buffer
+    size_t frames2_cap[2] = {0, 0};
+    int async_next = 0;
     unsigned long long* d_counters = nullptr;
     std::vector<EventPair> pending, pool;
     ncclComm_t comm = nullptr;
@@ -376,6 +379,8 @@ void rt_destroy(rt_ctx* ctx) {
         if (d.d_frame) (void)hipFree(d.d_frame);
         if (d.d_bands) (void)hipFree(d.d_bands);
         if (d.d_gather) (void)hipFree(d.d_gather);
+        for (int i = 0; i < 2; ++i)
+            if (d.d_frames2[i]) (void)hipFree(d.d_frames2[i]);
         if (d.d_counters) (void)hipFree(d.d_counters);
         if (d.stream) (void)hipStreamDestroy(d.stream);
     }
@@ -653,6 +658,95 @@ int rt_render(rt_ctx* ctx, int width, int height, int32_t* pixels) {
     ctx->frames++;
     ctx->pixels += (uint64_t)width * (uint64_t)height;
     return RT_OK;
+}
+
+// Double-buffered Tick(): trace into device buffer k % 2, D2H into the caller's buffer,
+// all on the context's stream (so frames complete in order); no host synchronisation.
+int rt_render_async(rt_ctx* ctx, int width, int height, int32_t* pixels) {
+    int rc = check_ctx(ctx, width, height);
+    if (rc != RT_OK) return rc;
+    if (!pixels) return fail(ctx, RT_ERR_INVALID_ARG, "NULL pixels");
+    if (ctx->n_gpus != 1) return rt_render(ctx, width, height, pixels);
+    Device& d = ctx->dev[0];
+    DeviceGuard guard(d.id);
+    const size_t frame_bytes = (size_t)width * height * sizeof(int32_t);
+    const int slot = d.async_next;
+    rc = grow(ctx, (void**)&d.d_frames2[slot], &d.frames2_cap[slot], frame_bytes);
+    if (rc != RT_OK) return rc;
+    rc = trace_bands(ctx, d, d.stream, width, height, height, 0, 1, d.d_frames2[slot], nullptr);
+    if (rc != RT_OK) return rc;
+    begin_timed(ctx, d, 1);
+    HIP_TRY(ctx, hipMemcpyAsync(pixels, d.d_frames2[slot], frame_bytes, hipMemcpyDeviceToHost, d.stream));
+    end_timed(d);
+    d.async_next = slot ^ 1;
+    ctx->frames++;
+    ctx->pixels += (uint64_t)width * (uint64_t)height;
+    return RT_OK;
+}
+
+int rt_wait(rt_ctx* ctx) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "NULL context");
+    for (Device& d : ctx->dev) {
+        DeviceGuard guard(d.id);
+        HIP_TRY(ctx, hipStreamSynchronize(d.stream));
+    }
+    return RT_OK;
+}
+
+// Debug ray view: re-trace every sample_stride-th pixel and append its segments.
+int rt_debug_segments(rt_ctx* ctx, int width, int height, int sample_stride, rt_segment* out, int capacity,
+                      int* out_count) {
+    int rc = check_ctx(ctx, width, height);
+    if (rc != RT_OK) return rc;
+    if (sample_stride <= 0 || capacity < 0 || (capacity > 0 && !out) || !out_count)
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_debug_segments: bad arguments");
+    static_assert(sizeof(rt_segment) == sizeof(DevSegment), "rt_segment layout");
+    Device& d = ctx->dev[0];
+    DeviceGuard guard(d.id);
+    LaunchParams lp;
+    std::memset(&lp, 0, sizeof lp);
+    rc = view_params(ctx, width, height, lp);
+    if (rc != RT_OK) return rc;
+    scene_params(ctx, d, lp);
+    lp.band_rows = height, lp.band_first = 0, lp.band_step = 1, lp.local_rows = height;
+    DevSegment* d_out = nullptr;
+    unsigned* d_count = nullptr;
+    HIP_TRY(ctx, hipMalloc((void**)&d_count, sizeof(unsigned)));
+    hipError_t e = hipMemset(d_count, 0, sizeof(unsigned));
+    if (e == hipSuccess && capacity > 0) e = hipMalloc((void**)&d_out, sizeof(DevSegment) * (size_t)capacity);
+    if (e == hipSuccess) e = (hipError_t)launch_debug_segments(lp, sample_stride, d_out, capacity, d_count, d.stream);
+    unsigned n = 0;
+    if (e == hipSuccess) e = hipMemcpyAsync(&n, d_count, sizeof n, hipMemcpyDeviceToHost, d.stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(d.stream);
+    const unsigned keep = n < (unsigned)capacity ? n : (unsigned)capacity;
+    if (e == hipSuccess && keep) e = hipMemcpy(out, d_out, sizeof(DevSegment) * keep, hipMemcpyDeviceToHost);
+    (void)hipFree(d_count);
+    if (d_out) (void)hipFree(d_out);
+    if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "rt_debug_segments: %s", hipGetErrorString(e));
+    *out_count = (int)n;
+    return RT_OK;
+}
+
+// Binary PPM (P6) of 0x00RRGGBB pixels -- the headless stand-in for the GL texture upload
+// (template.cs:188-193), also used to eyeball frames from tests.
+int rt_write_ppm(const char* path, const int32_t* pixels, int width, int height) {
+    if (!path || !pixels || width <= 0 || height <= 0) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_write_ppm: bad args");
+    FILE* f = std::fopen(path, "wb");
+    if (!f) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_write_ppm: cannot open %s", path);
+    std::fprintf(f, "P6\n%d %d\n255\n", width, height);
+    std::vector<unsigned char> row((size_t)width * 3);
+    bool ok = true;
+    for (int y = 0; y < height && ok; ++y) {
+        for (int x = 0; x < width; ++x) {
+            const uint32_t v = (uint32_t)pixels[(size_t)y * width + x];
+            row[(size_t)x * 3 + 0] = (unsigned char)(v >> 16);
+            row[(size_t)x * 3 + 1] = (unsigned char)(v >> 8);
+            row[(size_t)x * 3 + 2] = (unsigned char)v;
+        }
+        ok = std::fwrite(row.data(), 1, row.size(), f) == row.size();
+    }
+    ok = (std::fclose(f) == 0) && ok;
+    return ok ? RT_OK : fail(nullptr, RT_ERR_INVALID_ARG, "rt_write_ppm: write failed for %s", path);
 }
 
 int rt_get_stats(rt_ctx* ctx, rt_stats* out) {

@@ -88,7 +88,15 @@ struct LaunchParams {
     PrimConst pc[MAX_PRIM_CONST];
 };
 
+// Debug-view segment (layout of rt_segment in include/raytracer_hip.h).
+struct DevSegment {
+    float ox, oy, oz, ex, ey, ez;
+    int kind, pixel;
+};
+
 // Launchers (rt_kernel.hip).  Return hipError_t as int.
+int launch_debug_segments(const LaunchParams& p, int stride, DevSegment* out, int capacity, unsigned* count,
+                          void* stream);
 // generic_pow: some material needs the f64 Math.Pow path (exponent not 0.5, 1 or 2).
 int launch_trace(const LaunchParams& p, bool generic_pow, void* stream);
 int launch_scatter_bands(const int32_t* bands, int32_t* frame, int W, int H, int band_rows, int band_first,

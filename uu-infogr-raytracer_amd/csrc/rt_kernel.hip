@@ -896,6 +896,67 @@ __global__ __launch_bounds__(256) void trace_bundle_kernel(LaunchParams p) {
     }
 }
 
+// ---------------------------------------------------------------------------------
+// Debug ray view: re-trace sampled pixels with the direct path's
+// selection rules and append their visible-path segments.  Not on the timed path.
+// ---------------------------------------------------------------------------------
+__device__ __forceinline__ void append_segment(DevSegment* out, int cap, unsigned* count, f3 o, f3 e, int kind,
+                                               int pixel) {
+    const unsigned i = atomicAdd(count, 1u);
+    if (i < (unsigned)cap) out[i] = DevSegment{o.x, o.y, o.z, e.x, e.y, e.z, kind, pixel};
+}
+
+__global__ __launch_bounds__(256) void debug_segments_kernel(LaunchParams p, int stride, DevSegment* out, int cap,
+                                                             unsigned* count) {
+    const long long idx = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * (long long)stride;
+    if (idx >= (long long)p.W * p.H) return;
+    const int x = (int)(idx % p.W), y = (int)(idx / p.W);
+    const f3 cam = mk(p.cam[0], p.cam[1], p.cam[2]);
+    const float px = (float)x / (float)p.W - 0.5f;
+    const float py = (float)y / (float)p.H - 0.5f;
+    const f3 vp = add(add(add(cam, scale(mk(p.right[0], p.right[1], p.right[2]), px * p.pw)),
+                          scale(mk(p.up[0], p.up[1], p.up[2]), py * p.ph)),
+                      scale(mk(p.fwd[0], p.fwd[1], p.fwd[2]), 1.0f * p.nearc));
+    f3 d = normalize(sub(vp, cam));
+    f3 o = cam;
+    Hit h = nearest_direct<true, 0>(p, o, d);
+    for (int level = 0;; ++level) {
+        const bool none = h.prim == HIT_NONE;
+        append_segment(out, cap, count, o, add(o, scale(d, none ? 100.0f : h.t)), level == 0 ? 0 : 1,
+                       (int)idx);
+        if (none || h.t - 0.01f <= 0.0f || level > p.limit) break;
+        const bool is_sphere = h.prim >= 0;
+        const int prim = is_sphere ? h.prim : ~h.prim;
+        const f3 hp = add(o, scale(d, h.t));
+        const DevMaterial& m = p.mat[is_sphere ? prim : p.S + prim];
+        if (m.flags & MAT_DIFFUSE) {
+            for (int li = 0; li < p.L; ++li) {  // IntersectShadowLight's ray per light
+                const DevLight& l = p.li[li];
+                const bool l_ok = l.a2 > 0.0f && l.a2 < __builtin_inff();
+                const f3 lp = mk(l.px, l.py, l.pz);
+                float tb = 1.0f;
+                for (int i = 0; i < p.S; ++i) {
+                    if (shadow_blocked(hp, l, l_ok, p.sph[i])) {
+                        const f3 oc = sub(hp, mk(p.sph[i].cx, p.sph[i].cy, p.sph[i].cz));
+                        const float b = 2.0f * dot(oc, lp);
+                        const float c = dot(oc, oc) - p.sph[i].r2;
+                        const float sq = __builtin_sqrtf(b * b - l.a4 * c);
+                        tb = (-b - sq) / l.a2;
+                        break;
+                    }
+                }
+                append_segment(out, cap, count, hp, add(hp, scale(lp, tb)), 2, (int)idx);
+            }
+        }
+        if (!(m.flags & MAT_MIRROR)) break;
+        const f3 normal = is_sphere ? normalize(sub(hp, mk(p.sph[prim].cx, p.sph[prim].cy, p.sph[prim].cz)))
+                                    : mk(p.pl[prim].nx, p.pl[prim].ny, p.pl[prim].nz);
+        d = sub(d, scale(normal, 2.0f * dot(d, normal)));
+        o = hp;
+        h = nearest_direct<false, 0>(p, o, d);
+    }
+}
+
 // Reassemble packed row bands (rt_render_bands layout) into a row-major frame.
 __global__ __launch_bounds__(256) void scatter_bands_kernel(const int32_t* __restrict__ bands,
                                                             int32_t* __restrict__ frame, int W, int H, int band_rows,
@@ -945,6 +1006,15 @@ int launch_trace(const LaunchParams& p, bool generic_pow, void* stream) {
         if (bundle) launch_bundle<false>(p, grid, block, s);
         else launch_direct_loop<false>(p, grid, block, s);
     }
+    return (int)hipGetLastError();
+}
+
+int launch_debug_segments(const LaunchParams& p, int stride, DevSegment* out, int capacity, unsigned* count,
+                          void* stream) {
+    const long long n = ((long long)p.W * p.H + stride - 1) / stride;
+    if (n <= 0) return (int)hipSuccess;
+    hipLaunchKernelGGL(debug_segments_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, p,
+                       stride, out, capacity, count);
     return (int)hipGetLastError();
 }
 

@@ -16,12 +16,13 @@ import ctypes as C
 
 import numpy as np
 
-from . import abi, scenes
+from . import abi, debugview, scenes
 from .abi import RayTracerError, check, load_library
+from .debugview import SEGMENT_DTYPE, DebugView, surface_line
 from .dist import bands_of
 
 __all__ = ["Surface", "RayTracer", "Context", "RayTracerError", "scenes", "abi", "load_library",
-           "device_count", "camera_view", "bands_of"]
+           "device_count", "camera_view", "bands_of", "DebugView", "SEGMENT_DTYPE", "debugview"]
 
 
 def device_count() -> int:
@@ -48,6 +49,14 @@ class Surface:
 
     def Clear(self, c: int):  # surface.cs:43-46
         self.pixels[:] = np.int32(c)
+
+    def Line(self, x1: int, y1: int, x2: int, y2: int, c: int):  # surface.cs:57-100
+        surface_line(self.pixels, self.width, self.height, x1, y1, x2, y2, c)
+
+    def save_ppm(self, path: str):
+        """Headless display hand-off (rt_write_ppm): the frame as a binary PPM."""
+        lib = load_library()
+        check(lib, lib.rt_write_ppm(path.encode(), self.pixels.ctypes.data, self.width, self.height))
 
     def image(self) -> np.ndarray:
         return self.pixels.reshape(self.height, self.width)
@@ -124,6 +133,30 @@ class Context:
         self._check(self.lib.rt_scatter_bands(self.ptr, width, height, band_rows, band_first, band_step,
                                               C.c_void_p(d_bands), C.c_void_p(d_frame), C.c_void_p(stream)))
 
+    def render_async(self, width: int, height: int, out: np.ndarray):
+        """Double-buffered Tick (rt_render_async): returns at once; `wait()` before reading `out`."""
+        assert out.dtype == np.int32 and out.flags.c_contiguous and out.size == width * height
+        self._check(self.lib.rt_render_async(self.ptr, width, height, out.ctypes.data))
+
+    def wait(self):
+        self._check(self.lib.rt_wait(self.ptr))
+
+    def debug_segments(self, width: int, height: int, sample_stride: int = 0,
+                       capacity: int = 0) -> tuple[np.ndarray, int]:
+        """Visible-path segments of every `sample_stride`-th pixel (rt_debug_segments).
+        Returns (segments, total appended); total > len(segments) means the buffer was full.
+        sample_stride 0 picks one that samples about 4096 pixels."""
+        if sample_stride <= 0:
+            sample_stride = max(1, (width * height) // 4096)
+        if capacity <= 0:
+            n_pix = -(-(width * height) // sample_stride)
+            capacity = n_pix * 8
+        out = np.zeros(capacity, dtype=SEGMENT_DTYPE)
+        n = C.c_int(0)
+        self._check(self.lib.rt_debug_segments(self.ptr, width, height, sample_stride, out.ctypes.data,
+                                               capacity, C.byref(n)))
+        return out[:min(n.value, capacity)], n.value
+
     def register_host(self, arr: np.ndarray):
         self._check(self.lib.rt_register_host(self.ptr, C.c_void_p(arr.ctypes.data), arr.nbytes))
 
@@ -144,15 +177,21 @@ class RayTracer:
     """RayTracer.cs:437-1062, public surface only, rendering on MI355X.
 
     `scene` defaults to the reference's hard-coded scene (RayTracer.cs:441-490).
+    `debug=True` is the reference's DEBUG_ENABLE build: Tick() also composites the top-down
+    ray inset (raytracer_hip.debugview) into the bottom-right corner of the frame.
     """
 
     _KEYS = {"W": abi.RT_KEY_W, "A": abi.RT_KEY_A, "S": abi.RT_KEY_S, "D": abi.RT_KEY_D,
              "Space": abi.RT_KEY_SPACE, "LeftShift": abi.RT_KEY_SHIFT, "RightShift": abi.RT_KEY_SHIFT}
 
-    def __init__(self, screen: Surface, scene: scenes.Scene | None = None, n_gpus: int = 1):
+    def __init__(self, screen: Surface, scene: scenes.Scene | None = None, n_gpus: int = 1,
+                 debug: bool = False, debug_seed: int = 0):
         self.screen = screen
+        self.debug = debug
+        self._debug_seed = debug_seed
         self._ctx = Context(n_gpus)
         sc = scene or scenes.reference(screen.width, screen.height)
+        self._scene = sc
         self._ctx.set_scene(sc)
         self._camera = sc.c_camera()
         self._ctx.register_host(screen.pixels)  # pin Surface.pixels once (D2H lands in it)
@@ -161,6 +200,12 @@ class RayTracer:
         """RayTracer.Tick(), RayTracer.cs:886-935: the whole frame, synchronously."""
         self._ctx.set_camera(self._camera)
         self._ctx.render(self.screen.width, self.screen.height, self.screen.pixels)
+        if self.debug:
+            w, h = self.screen.width, self.screen.height
+            segs, _ = self._ctx.debug_segments(w, h)
+            DebugView(w, h).compose(self.screen.pixels, self._camera.position.tuple(), self._scene.spheres, segs,
+                                    seed=self._debug_seed)
+            self._debug_seed += 1
 
     def OnKeyPress(self, key):
         """RayTracer.OnKeyPress, RayTracer.cs:543-554 (key: 'W','A','S','D','Space','LeftShift'...)."""

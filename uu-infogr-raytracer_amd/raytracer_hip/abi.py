@@ -60,6 +60,10 @@ class rt_view(C.Structure):
     ]
 
 
+class rt_segment(C.Structure):
+    _fields_ = [("origin", rt_vec3), ("end", rt_vec3), ("kind", C.c_int32), ("pixel", C.c_int32)]
+
+
 class rt_stats(C.Structure):
     _fields_ = [
         ("frames", C.c_uint64), ("pixels", C.c_uint64), ("primary_rays", C.c_uint64),
@@ -94,6 +98,10 @@ EXPORTS = [
                                   C.c_void_p, C.POINTER(C.c_int)]),
     ("rt_scatter_bands", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                    C.c_void_p, C.c_void_p]),
+    ("rt_render_async", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
+    ("rt_wait", C.c_int, [C.c_void_p]),
+    ("rt_write_ppm", C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),
+    ("rt_debug_segments", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_int)]),
     ("rt_get_stats", C.c_int, [C.c_void_p, C.POINTER(rt_stats)]),
     ("rt_reset_stats", C.c_int, [C.c_void_p]),
 ]
