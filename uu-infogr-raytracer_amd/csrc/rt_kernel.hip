@@ -236,7 +236,8 @@ struct HybridStack {
         b0 = y;
         ++n;
     }
-    __device__ __forceinline__ void pop(float4& x, float4& y) {
+    __device__ __forceinline__ void origin(f3) {}
+    __device__ __forceinline__ void pop(const LaunchParams&, float4& x, float4& y) {
         x = a0;
         y = b0;
         a0 = a1;
@@ -253,29 +254,156 @@ struct NoOverflow {};
 template <int K, bool SCRATCH>
 struct PlainStack : LevelStack<K, SCRATCH> {
     __device__ __forceinline__ explicit PlainStack(NoOverflow*) {}
+    __device__ __forceinline__ void origin(f3) {}
+    __device__ __forceinline__ void pop(const LaunchParams&, float4& x, float4& y) { LevelStack<K, SCRATCH>::pop(x, y); }
 };
 
-// Stack type per K: registers up to 2 records, hybrid up to 8, scratch beyond.
+// One reflection step of the forward walk (TraceSphere :854 / TracePlane normal,
+// CalculateReflectionRay :718-720): hit point of segment (o, d) at t, then the reflected
+// segment.  The walks and the compact stacks' re-walk share it, so the re-walk reproduces
+// every hit point and direction bit for bit.
+__device__ __forceinline__ f3 reflect_at(const LaunchParams& p, f3 o, f3& d, float t, int code) {
+    const f3 hp = add(o, scale(d, t));
+    f3 normal;
+    if (code >= 0) {
+        const DevSphere& s = p.sph[code];
+        normal = normalize(sub(hp, mk(s.cx, s.cy, s.cz)));
+    } else {
+        const DevPlane& pl = p.pl[~code];
+        normal = mk(pl.nx, pl.ny, pl.nz);
+    }
+    d = sub(d, scale(normal, 2.0f * dot(d, normal)));
+    return hp;
+}
+
+// Compact stacks: a record is fully determined by the camera ray and the (t, primitive)
+// pairs of the levels above it, so older levels keep only those 8 bytes (registers,
+// statically indexed) and are rebuilt by re-walking the reflection chain -- no scratch
+// traffic at all.
+// RT_STACK 1: every level compact, each pop re-walks (level k costs k steps).  The levels
+// live in register vectors; the re-walk loop is rolled with a wave-uniform index (indirect
+// register reads, no scratch), the per-lane top is picked by a select chain.
+template <int K>
+struct CompactStack {
+    typedef float tvec __attribute__((ext_vector_type(K)));
+    typedef int cvec __attribute__((ext_vector_type(K)));
+    tvec t;
+    cvec c;
+    f3 d0;
+    int n = 0;
+    __device__ __forceinline__ explicit CompactStack(NoOverflow*) {}
+    __device__ __forceinline__ void origin(f3 d) { d0 = d; }
+    __device__ __forceinline__ void push(float4 x, float4 y) {
+#pragma unroll
+        for (int i = 0; i < K; ++i)
+            if (i == n) {
+                t[i] = x.w;
+                c[i] = __float_as_int(y.w);
+            }
+        ++n;
+    }
+    __device__ __forceinline__ void pop(const LaunchParams& p, float4& x, float4& y) {
+        --n;
+        f3 o = mk(p.cam[0], p.cam[1], p.cam[2]), d = d0;
+#pragma unroll 1
+        for (int j = 0; j < K - 1; ++j) {
+            const bool go = j < n;
+            if (__builtin_amdgcn_ballot_w64(go) == 0) break;
+            if (go) o = reflect_at(p, o, d, t[j], c[j]);
+        }
+        float tk = t[0];
+        int ck = c[0];
+#pragma unroll
+        for (int i = 1; i < K; ++i)
+            if (i == n) {
+                tk = t[i];
+                ck = c[i];
+            }
+        const f3 hp = add(o, scale(d, tk));
+        x = make_float4(hp.x, hp.y, hp.z, tk);
+        y = make_float4(d.x, d.y, d.z, __int_as_float(ck));
+    }
+};
+
+// RT_STACK 2: the two most recent records whole in VGPRs, older levels compact; only the
+// refill of the second record re-walks (levels n-3.. of an n-deep chain).
+template <int K>
+struct CompactHybridStack {
+    float4 a0, b0, a1, b1;
+    float t[K - 2];
+    int c[K - 2];
+    f3 d0;
+    int n = 0;
+    __device__ __forceinline__ explicit CompactHybridStack(NoOverflow*) {}
+    __device__ __forceinline__ void origin(f3 d) { d0 = d; }
+    __device__ __forceinline__ void push(float4 x, float4 y) {
+        if (n >= 2) {
+#pragma unroll
+            for (int i = 0; i < K - 2; ++i)
+                if (i == n - 2) {
+                    t[i] = a1.w;
+                    c[i] = __float_as_int(b1.w);
+                }
+        }
+        a1 = a0;
+        b1 = b0;
+        a0 = x;
+        b0 = y;
+        ++n;
+    }
+    __device__ __forceinline__ void pop(const LaunchParams& p, float4& x, float4& y) {
+        x = a0;
+        y = b0;
+        a0 = a1;
+        b0 = b1;
+        --n;
+        if (n >= 2) {  // rebuild level n-2 from the compact levels 0..n-2
+            f3 o = mk(p.cam[0], p.cam[1], p.cam[2]), d = d0;
+            float tk = t[0];
+            int ck = c[0];
+#pragma unroll
+            for (int j = 0; j < K - 3; ++j)
+                if (j < n - 2) {
+                    o = reflect_at(p, o, d, t[j], c[j]);
+                    tk = t[j + 1];
+                    ck = c[j + 1];
+                }
+            const f3 hp = add(o, scale(d, tk));
+            a1 = make_float4(hp.x, hp.y, hp.z, tk);
+            b1 = make_float4(d.x, d.y, d.z, __int_as_float(ck));
+        }
+    }
+};
+
+#ifndef RT_STACK
+#define RT_STACK 1
+#endif
+template <int K>
+struct MidStack {  // stack for K = 4, 6, 8
+#if RT_STACK == 1
+    using type = CompactStack<K>;
+    using overflow = NoOverflow;
+#elif RT_STACK == 2
+    using type = CompactHybridStack<K>;
+    using overflow = NoOverflow;
+#else
+    using type = HybridStack<K>;
+    using overflow = HybridOverflow<K>;
+#endif
+};
+
+// Stack type per K: registers up to 2 records, MidStack up to 8, scratch beyond.
 template <int K, bool SCRATCH>
 struct StackFor {
     using type = PlainStack<K, SCRATCH>;
     using overflow = NoOverflow;
 };
 template <>
-struct StackFor<4, false> {
-    using type = HybridStack<4>;
-    using overflow = HybridOverflow<4>;
-};
+struct StackFor<4, false> : MidStack<4> {};
 template <>
-struct StackFor<6, false> {
-    using type = HybridStack<6>;
-    using overflow = HybridOverflow<6>;
-};
+struct StackFor<6, false> : MidStack<6> {};
 template <>
-struct StackFor<8, false> {
-    using type = HybridStack<8>;
-    using overflow = HybridOverflow<8>;
-};
+struct StackFor<8, false> : MidStack<8> {};
 
 __device__ __forceinline__ unsigned wave_sum(unsigned v) {
 #pragma unroll
@@ -448,6 +576,7 @@ __global__ __launch_bounds__(256) void trace_direct_kernel(LaunchParams p) {
 
         typename StackFor<K, SCRATCH>::overflow ovf;
         typename StackFor<K, SCRATCH>::type stk(&ovf);
+        stk.origin(d);
         f3 leaf = mk(0.0f, 0.0f, 0.0f);
         Hit h = nearest_direct<true, SMAX>(p, o, d);
         int count = 0;
@@ -465,16 +594,7 @@ __global__ __launch_bounds__(256) void trace_direct_kernel(LaunchParams p) {
             const int prim = is_sphere ? h.prim : ~h.prim;
             const uint32_t flags = p.mat[is_sphere ? prim : p.S + prim].flags;
             if (!(flags & MAT_MIRROR) || RT_ABLATE == 3) break;
-            f3 normal;
-            if (is_sphere) {
-                const DevSphere& s = p.sph[prim];
-                normal = normalize(sub(hp, mk(s.cx, s.cy, s.cz)));  // :854
-            } else {
-                const DevPlane& pl = p.pl[prim];
-                normal = mk(pl.nx, pl.ny, pl.nz);
-            }
-            d = sub(d, scale(normal, 2.0f * dot(d, normal)));  // CalculateReflectionRay :718-720
-            o = hp;
+            o = reflect_at(p, o, d, h.t, h.prim);  // :854, CalculateReflectionRay :718-720
             ++count;
             ++n_refl;
             h = nearest_direct<false, SMAX>(p, o, d);
@@ -486,13 +606,13 @@ __global__ __launch_bounds__(256) void trace_direct_kernel(LaunchParams p) {
         if constexpr (RT_ABLATE == 1) {  // keep the walk alive: fold the records' t into the colour
             while (stk.n > 0) {
                 float4 ra, rb;
-                stk.pop(ra, rb);
+                stk.pop(p, ra, rb);
                 col.x += ra.w;
             }
         }
         while (RT_ABLATE != 1 && stk.n > 0) {
             float4 ra, rb;
-            stk.pop(ra, rb);
+            stk.pop(p, ra, rb);
             const int code = __float_as_int(rb.w);
             const bool is_s = code >= 0;
             col = shade_direct<GPOW, SMAX>(p, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z), ra.w, col,
@@ -809,6 +929,7 @@ __global__ __launch_bounds__(256) void trace_bundle_kernel(LaunchParams p) {
     // shaded hit pushes a record; mirror hits continue with the reflected segment
     typename StackFor<K, SCRATCH>::overflow ovf;
     typename StackFor<K, SCRATCH>::type stk(&ovf);
+        stk.origin(d);
     f3 leaf = mk(0.0f, 0.0f, 0.0f);
     bool active = valid;
     Hit h = nearest_bundle<true>(p, o, d, active);
@@ -828,16 +949,7 @@ __global__ __launch_bounds__(256) void trace_bundle_kernel(LaunchParams p) {
                 if (!(flags & MAT_MIRROR)) {
                     active = false;
                 } else {
-                    f3 normal;
-                    if (is_sphere) {
-                        const DevSphere& s = p.sph[prim];
-                        normal = normalize(sub(hp, mk(s.cx, s.cy, s.cz)));  // :854
-                    } else {
-                        const DevPlane& pl = p.pl[prim];
-                        normal = mk(pl.nx, pl.ny, pl.nz);
-                    }
-                    d = sub(d, scale(normal, 2.0f * dot(d, normal)));  // CalculateReflectionRay :718-720
-                    o = hp;
+                    o = reflect_at(p, o, d, h.t, h.prim);  // :854, CalculateReflectionRay :718-720
                     ++n_refl;
                 }
             }
@@ -855,7 +967,7 @@ __global__ __launch_bounds__(256) void trace_bundle_kernel(LaunchParams p) {
     while (level-- > 0) {
         const bool act = level < depth;  // this lane's top record is at `level`
         float4 ra = make_float4(0.0f, 0.0f, 0.0f, 1.0f), rb = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
-        if (act) stk.pop(ra, rb);
+        if (act) stk.pop(p, ra, rb);
         const unsigned long long am = __builtin_amdgcn_ballot_w64(act);
         if (am != ~0ull) {  // idle lanes shade a copy of the first active lane's record
             const int ref = __builtin_ctzll(am);
