@@ -89,7 +89,7 @@ struct Device {
 
 struct SceneLayout {
     int S = 0, P = 0, L = 0, limit = 0;
-    size_t off_sph = 0, off_mat = 0, off_pl = 0, off_li = 0, bytes = 0;
+    size_t off_sph = 0, off_mat = 0, off_pl = 0, off_li = 0, off_cull = 0, bytes = 0;
     bool generic_pow = false;        // a specular material with n not in {0.5, 1, 2}
     std::vector<DevSphere> host_sph;  // for the per-frame primary constants
 };
@@ -251,6 +251,7 @@ void scene_params(const rt_ctx* ctx, const Device& d, LaunchParams& lp) {
     lp.mat = (const DevMaterial*)(base + L.off_mat);
     lp.pl = (const DevPlane*)(base + L.off_pl);
     lp.li = (const DevLight*)(base + L.off_li);
+    lp.scull = (const DevSphereCull*)(base + L.off_cull);
     lp.S = L.S, lp.P = L.P, lp.L = L.L, lp.limit = L.limit;
     lp.counters = d.d_counters;
 }
@@ -405,17 +406,22 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
     L.off_mat = al(L.off_sph + sizeof(DevSphere) * (size_t)n_spheres);
     L.off_pl = al(L.off_mat + sizeof(DevMaterial) * (size_t)(n_spheres + n_planes));
     L.off_li = al(L.off_pl + sizeof(DevPlane) * (size_t)n_planes);
-    L.bytes = al(L.off_li + sizeof(DevLight) * (size_t)n_lights) + 256;
+    L.off_cull = al(L.off_li + sizeof(DevLight) * (size_t)n_lights);
+    L.bytes = al(L.off_cull + sizeof(DevSphereCull) * (size_t)n_spheres) + 256;
 
     std::vector<unsigned char> blob(L.bytes, 0);
     DevSphere* sph = (DevSphere*)(blob.data() + L.off_sph);
     DevMaterial* mat = (DevMaterial*)(blob.data() + L.off_mat);
     DevPlane* pl = (DevPlane*)(blob.data() + L.off_pl);
     DevLight* li = (DevLight*)(blob.data() + L.off_li);
+    DevSphereCull* cull = (DevSphereCull*)(blob.data() + L.off_cull);
     for (int i = 0; i < n_spheres; ++i) {
         const rt_sphere& s = spheres[i];
         sph[i] = DevSphere{s.center.x, s.center.y, s.center.z, s.radius * s.radius};  // :336
         mat[i] = dev_material(s.material, ambient);
+        // cull radius: an upper bound of sqrt(r^2) (1 + 2^-8), rounded up (NaN stays NaN)
+        const double rr = std::sqrt((double)sph[i].r2) * (1.0 + 0x1p-8);
+        cull[i] = DevSphereCull{sph[i].cx, sph[i].cy, sph[i].cz, std::nextafter((float)rr, INFINITY)};
     }
     L.host_sph.assign(sph, sph + n_spheres);
     for (int i = 0; i < n_planes; ++i) {
@@ -443,6 +449,18 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
         d.a = hdot(p, p);  // IntersectsSphere's a = Dot(direction, direction), :617
         d.a2 = 2.0f * d.a;
         d.a4 = 4.0f * d.a;
+        // shadow-cull frame (kernel uses it only when a is in [2^-40, 2^40])
+        const double len = std::sqrt((double)p.x * p.x + (double)p.y * p.y + (double)p.z * p.z);
+        double A[3] = {0.0, 0.0, 1.0};
+        if (len > 0 && std::isfinite(len)) A[0] = p.x / len, A[1] = p.y / len, A[2] = p.z / len;
+        const double h[3] = {std::fabs(A[0]) < 0.9 ? 1.0 : 0.0, std::fabs(A[0]) < 0.9 ? 0.0 : 1.0, 0.0};
+        double U[3] = {A[1] * h[2] - A[2] * h[1], A[2] * h[0] - A[0] * h[2], A[0] * h[1] - A[1] * h[0]};
+        const double ul = std::sqrt(U[0] * U[0] + U[1] * U[1] + U[2] * U[2]);
+        for (double& c : U) c /= ul;
+        const double V[3] = {A[1] * U[2] - A[2] * U[1], A[2] * U[0] - A[0] * U[2], A[0] * U[1] - A[1] * U[0]};
+        d.ax = (float)A[0], d.ay = (float)A[1], d.az = (float)A[2];
+        d.ux = (float)U[0], d.uy = (float)U[1], d.uz = (float)U[2];
+        d.vx = (float)V[0], d.vy = (float)V[1], d.vz = (float)V[2];
         li[i] = d;
     }
     for (int i = 0; i < n_spheres + n_planes; ++i)

@@ -48,6 +48,16 @@ struct DevLight {
     float a2;     // 2 * a
     float a4;     // 4 * a
     float pad;
+    // shadow-cull frame (culling only, never in a result): A ~ p/|p| (every shadow ray of this
+    // light has direction p), U, V ~ orthonormal to A
+    float ax, ay, az, pad1;
+    float ux, uy, uz, pad2;
+    float vx, vy, vz, pad3;
+};
+
+// Per-sphere culling record: centre and a radius bound r' >= sqrt(r^2) * (1 + 2^-8).
+struct DevSphereCull {
+    float cx, cy, cz, rr;
 };
 
 // Work counters: each workgroup adds its totals into slot (block id % COUNTER_SLOTS) so that
@@ -74,6 +84,7 @@ struct LaunchParams {
     const DevMaterial* mat;  // [S + P]
     const DevPlane* pl;
     const DevLight* li;
+    const DevSphereCull* scull;  // [S]
     int S, P, L, limit;
     // view, RayTracer.cs:511-523 and :892-896 (computed on the host)
     float cam[3], right[3], up[3], fwd[3];

@@ -29,6 +29,11 @@
 #ifndef RT_ABLATE
 #define RT_ABLATE 0
 #endif
+// RT_CULLSTATS (experiments only): the bundle kernel's reflect/shadow counters count the
+// wave-iterations of its shadow exact-test loops (1) or its shadow bundles (2) instead of rays.
+#ifndef RT_CULLSTATS
+#define RT_CULLSTATS 0
+#endif
 
 namespace rtk {
 
@@ -758,6 +763,78 @@ __device__ __forceinline__ unsigned long long cull_mask(const LaunchParams& p, c
     return __builtin_amdgcn_ballot_w64(cand);
 }
 
+// Shadow bundles.  Every shadow ray of light l has the same direction p_l (the light
+// POSITION, Q2), so a sphere can block lane k only if the line {hp_k + s p_l} passes within
+// r of its centre: a 2-D test in the light's frame (U, V, A ~ p_l/|p_l|, host-built), where
+// the wave's hit points spread by R_perp across A and by [-R_neg, R_pos] along it.  Cull
+// rules (same error analysis and 2^-8 margin as cull_mask, with |u| bounded by the L1 norm
+// of the frame coordinates plus the spreads): line miss if |w_perp| - R_perp > r' + mgn;
+// behind (b >= 0 for every lane) if -w_A - R_neg > mgn, where w = C - O.
+#ifndef RT_SHADOW_CULL
+#define RT_SHADOW_CULL 1
+#endif
+struct ShadowBundle {
+    f3 O;
+    float Rp, Rneg, Rsum;  // perpendicular spread, backward spread, Rp + Rneg + Rpos
+    bool ok;
+};
+
+__device__ __forceinline__ ShadowBundle make_shadow_bundle(f3 hp, const DevLight& l, bool active) {
+    ShadowBundle B;
+    const unsigned long long m = __builtin_amdgcn_ballot_w64(active);
+    B.ok = false;
+    B.Rp = B.Rneg = B.Rsum = 0.0f;
+    B.O = hp;
+    if (m == 0) return B;
+    B.O = readlane3(hp, __builtin_ctzll(m));
+    float perp2 = 0.0f, neg = 0.0f, pos = 0.0f;
+    bool bad = false;
+    if (active) {
+        const f3 e = sub(hp, B.O);
+        const float eu = dot(e, mk(l.ux, l.uy, l.uz));
+        const float ev = dot(e, mk(l.vx, l.vy, l.vz));
+        const float ea = dot(e, mk(l.ax, l.ay, l.az));
+        perp2 = eu * eu + ev * ev;
+        neg = nmax0(-ea);
+        pos = nmax0(ea);
+        bad = !(perp2 < 0x1p80f) || !(neg < 0x1p40f) || !(pos < 0x1p40f);  // also NaN / inf
+    }
+    bad = __builtin_amdgcn_ballot_w64(bad) != 0;
+    const float Rp2 = wave_max(perp2);
+    B.Rp = __builtin_sqrtf(Rp2) * (1.0f + 0x1p-10f) + 0x1p-60f;
+    B.Rneg = wave_max(neg) * (1.0f + 0x1p-10f) + 0x1p-60f;
+    const float Rpos = wave_max(pos) * (1.0f + 0x1p-10f) + 0x1p-60f;
+    B.Rsum = B.Rp + B.Rneg + Rpos;
+    B.ok = !bad && l.a >= 0x1p-40f && l.a <= 0x1p40f && l.a2 < __builtin_inff() && B.Rsum < 0x1p41f;
+    return B;
+}
+
+// Candidate mask of spheres [base, base+n) (n <= 64) for shadow bundle B.  Converged call.
+__device__ __forceinline__ unsigned long long shadow_cull_mask(const LaunchParams& p, const ShadowBundle& B,
+                                                               const DevLight& l, int base, int n) {
+    const int lane = threadIdx.x & 63;
+    bool cand = false;
+    if (lane < n) {
+        cand = true;
+        if (B.ok) {
+            const DevSphereCull s = p.scull[base + lane];
+            const f3 w = sub(mk(s.cx, s.cy, s.cz), B.O);
+            const float wu = dot(w, mk(l.ux, l.uy, l.uz));
+            const float wv = dot(w, mk(l.vx, l.vy, l.vz));
+            const float wa = dot(w, mk(l.ax, l.ay, l.az));
+            const float dc = __builtin_fabsf(wu) + __builtin_fabsf(wv) + __builtin_fabsf(wa);  // >= |w|
+            if (s.rr >= 0x1p-50f && dc >= 0x1p-30f && dc < 0x1p40f) {
+                const float mgn = 0x1p-8f * (dc + B.Rsum);
+                const float T = B.Rp + s.rr + mgn;
+                const bool line = wu * wu + wv * wv > T * T;
+                const bool behind = -wa - B.Rneg > mgn;
+                cand = !(line || behind);  // NaN anywhere -> candidate
+            }
+        }
+    }
+    return __builtin_amdgcn_ballot_w64(cand);
+}
+
 // BUNDLE path.  Nearest hit of one segment for every active lane (converged call).  PRIMARY: TracePixel's
 // rule (:977, :987, :993) with the per-frame camera-relative constants; otherwise
 // TraceSecondaryRay's asymmetric rule (:804-806, :819-821, :825).
@@ -861,16 +938,26 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
             const DevLight& l = p.li[li];
             const f3 lp = mk(l.px, l.py, l.pz);
             const bool l_ok = l.a2 > 0.0f && l.a2 < __builtin_inff();  // wave-uniform
+#if RT_SHADOW_CULL
+            const ShadowBundle B = make_shadow_bundle(hp, l, diff);
+#else
             Bundle B = make_bundle(hp, lp, diff, true);
             B.ok = B.ok && l_ok && l.a >= 0x1p-40f && l.a <= 0x1p40f;
+#endif
             const f3 hs = diff ? hp : B.O;  // idle lanes mirror a shading lane (results ignored)
             bool blocked = !diff;
-            for (int base = 0; base < p.S; base += 64) {
+            if constexpr (RT_CULLSTATS == 2) *n_shadow += (threadIdx.x & 63) == 0;
+            for (int base = 0; RT_ABLATE != 2 && base < p.S; base += 64) {
                 const int n = min(64, p.S - base);
+#if RT_SHADOW_CULL
+                unsigned long long mk64 = shadow_cull_mask(p, B, l, base, n);
+#else
                 unsigned long long mk64 = cull_mask(p, B, base, n);
+#endif
                 while (mk64) {
                     const int i = base + (int)__builtin_ctzll(mk64);
                     mk64 &= mk64 - 1;
+                    if constexpr (RT_CULLSTATS == 1) *n_shadow += (threadIdx.x & 63) == 0;
                     blocked = blocked | shadow_blocked(hs, l, l_ok, p.sph[i]);  // no short-circuit branch
                     if (__builtin_amdgcn_ballot_w64(!blocked) == 0) break;
                 }
@@ -895,7 +982,7 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
             }
             if (diff) col = add(col, term);
         }
-        if (diff) *n_shadow += (unsigned)p.L;
+        if (diff && !RT_CULLSTATS) *n_shadow += (unsigned)p.L;
     }
     col = add(col, mk(m.amb[0], m.amb[1], m.amb[2]));
     return act ? col : sec;
@@ -946,7 +1033,7 @@ __global__ __launch_bounds__(256) void trace_bundle_kernel(LaunchParams p) {
                 stk.push(make_float4(hp.x, hp.y, hp.z, h.t), make_float4(d.x, d.y, d.z, __int_as_float(h.prim)));
                 const int prim = is_sphere ? h.prim : ~h.prim;
                 const uint32_t flags = p.mat[is_sphere ? prim : p.S + prim].flags;
-                if (!(flags & MAT_MIRROR)) {
+                if (!(flags & MAT_MIRROR) || RT_ABLATE == 3) {
                     active = false;
                 } else {
                     o = reflect_at(p, o, d, h.t, h.prim);  // :854, CalculateReflectionRay :718-720
@@ -964,6 +1051,14 @@ __global__ __launch_bounds__(256) void trace_bundle_kernel(LaunchParams p) {
     f3 col = leaf;
     const int depth = stk.n;
     int level = (int)wave_max((float)depth);
+    if constexpr (RT_ABLATE == 1) {  // keep the walk alive: fold the records' t into the colour
+        while (stk.n > 0) {
+            float4 ra, rb;
+            stk.pop(p, ra, rb);
+            col.x += ra.w;
+        }
+        level = 0;
+    }
     while (level-- > 0) {
         const bool act = level < depth;  // this lane's top record is at `level`
         float4 ra = make_float4(0.0f, 0.0f, 0.0f, 1.0f), rb = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
