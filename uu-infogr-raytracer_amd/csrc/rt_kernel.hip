@@ -699,6 +699,26 @@ __device__ __forceinline__ float wave_max(float v) {
     return __uint_as_float(max(max(a, b), max(c, d)));
 }
 __device__ __forceinline__ float len3(f3 v) { return __builtin_sqrtf(dot(v, v)); }
+// Culling-only arithmetic (never feeds a result): hardware sqrt / rsq (about 1 ulp) instead of
+// the correctly rounded sequences; the cull margins (2^-10 relative on R and delta, 2^-8 on
+// the tests) are orders of magnitude above that error.
+#ifndef RT_FAST_CULL
+#define RT_FAST_CULL 1
+#endif
+__device__ __forceinline__ float clen3(f3 v) {
+#if RT_FAST_CULL
+    return __builtin_amdgcn_sqrtf(dot(v, v));
+#else
+    return len3(v);
+#endif
+}
+__device__ __forceinline__ f3 cnormalize(f3 v) {
+#if RT_FAST_CULL
+    return scale(v, __builtin_amdgcn_rsqf(dot(v, v)));
+#else
+    return normalize(v);
+#endif
+}
 __device__ __forceinline__ f3 cross3(f3 l, f3 r) {
     return mk(l.y * r.z - l.z * r.y, l.z * r.x - l.x * r.z, l.x * r.y - l.y * r.x);
 }
@@ -719,15 +739,15 @@ __device__ __forceinline__ Bundle make_bundle(f3 o, f3 d, bool active, bool dir_
     const int ref = __builtin_ctzll(m);
     B.O = readlane3(o, ref);
     const f3 dref = readlane3(d, ref);
-    B.A = normalize(dref);
+    B.A = cnormalize(dref);
     float e = 0.0f, f = 0.0f;
     bool bad = false;
     if (active) {
-        e = len3(sub(o, B.O));
+        e = clen3(sub(o, B.O));
         bad = !(e < 0x1p40f);  // also NaN / inf origins
         if (!dir_uniform) {
             const float a = dot(d, d);
-            f = len3(sub(normalize(d), B.A));
+            f = clen3(sub(cnormalize(d), B.A));
             bad = bad || !(a >= 0.5f && a <= 2.0f) || !(f < 2.0f);
         }
     }
@@ -747,13 +767,21 @@ __device__ __forceinline__ unsigned long long cull_mask(const LaunchParams& p, c
     if (lane < n) {
         cand = true;
         if (B.ok) {
+#if RT_FAST_CULL
+            const DevSphereCull s = p.scull[base + lane];
+            const f3 w = sub(mk(s.cx, s.cy, s.cz), B.O);
+            const float dc = clen3(w) * (1.0f + 0x1p-20f);
+            if (s.rr >= 0x1p-50f && dc >= 0x1p-30f && dc < 0x1p40f) {
+                const float rr = s.rr;
+#else
             const DevSphere s = p.sph[base + lane];
             const f3 w = sub(mk(s.cx, s.cy, s.cz), B.O);
             const float dc = len3(w);
             if (s.r2 >= 0x1p-100f && dc >= 0x1p-30f && dc < 0x1p40f) {
                 const float rr = __builtin_sqrtf(s.r2) * (1.0f + 0x1p-8f);
+#endif
                 const float mgn = 0x1p-8f * (dc + B.R);
-                const float x = len3(cross3(w, B.A));
+                const float x = clen3(cross3(w, B.A));
                 const bool line = (x - dc * B.delta - B.R) > rr + mgn;
                 const bool behind = (-dot(w, B.A) - dc * B.delta - B.R * (1.0f + B.delta)) > mgn;
                 cand = !(line || behind);  // NaN anywhere -> candidate
