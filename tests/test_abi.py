@@ -52,11 +52,11 @@ def test_struct_layouts_match_header():
     assert C.sizeof(abi.rt_plane) == 76
     assert C.sizeof(abi.rt_light) == 16
     assert C.sizeof(abi.rt_camera) == 20
-    assert C.sizeof(abi.rt_stats) == 8 * 8 + 4 * 8
+    assert C.sizeof(abi.rt_stats) == 8 * 8 + 4 * 8 + 3 * 8
 
 
 def test_abi_version(rtlib):
-    assert rtlib.rt_abi_version() == 1
+    assert rtlib.rt_abi_version() == 2
 
 
 def test_camera_view_matches_oracle(rtlib, oracle):
@@ -112,6 +112,8 @@ def test_null_arguments_are_errors(rtlib):
     assert rtlib.rt_set_scene(None, None, 0, None, 0, None, 0, abi.rt_vec3(0, 0, 0), 0) == abi.RT_ERR_INVALID_ARG
     assert rtlib.rt_render(None, 4, 4, None) == abi.RT_ERR_INVALID_ARG
     assert rtlib.rt_create(0, C.byref(C.c_void_p())) == abi.RT_ERR_INVALID_ARG
+    assert rtlib.rt_set_timing(None, 1) == abi.RT_ERR_INVALID_ARG
+    assert rtlib.rt_debug_segments(None, 4, 4, 1, None, 0, C.byref(C.c_int())) == abi.RT_ERR_INVALID_ARG
 
 
 def test_no_cpu_fallback_without_gpu(rtlib):
@@ -171,3 +173,27 @@ def test_write_ppm_roundtrip(tmp_path):
     assert (rgb[:, 0] == (u >> 16) & 255).all() and (rgb[:, 1] == (u >> 8) & 255).all() and (rgb[:, 2] == u & 255).all()
     lib = abi.load_library()
     assert lib.rt_write_ppm(None, None, 1, 1) == abi.RT_ERR_INVALID_ARG
+
+
+def test_ctypes_layouts_match_the_c_header(tmp_path):
+    """sizeof/offsetof of every ABI struct, from gcc on include/raytracer_hip.h, against the
+    ctypes mirror (what the C#/Go/Python bindings must reproduce)."""
+    import subprocess
+    structs = {n: getattr(abi, n) for n in ("rt_vec3", "rt_material", "rt_sphere", "rt_plane", "rt_light",
+                                           "rt_camera", "rt_view", "rt_segment", "rt_stats")}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "raytracer_hip.h"', "int main(void) {"]
+    for n, t in structs.items():
+        lines.append(f'printf("{n} %zu\\n", sizeof({n}));')
+        for f, _ in t._fields_:
+            lines.append(f'printf("{n}.{f} %zu\\n", offsetof({n}, {f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(l.split() for l in subprocess.run([str(exe)], capture_output=True, text=True,
+                                                  check=True).stdout.splitlines())
+    for n, t in structs.items():
+        assert int(got[n]) == C.sizeof(t), n
+        for f, _ in t._fields_:
+            assert int(got[f"{n}.{f}"]) == getattr(t, f).offset, f"{n}.{f}"

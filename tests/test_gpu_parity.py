@@ -209,8 +209,25 @@ def test_stats_accumulate_and_reset(gpu_ctx, golden):
     assert st["primary_rays"] == 3 * e["stats"]["primary_rays"]
     assert st["sphere_tests"] == (st["primary_rays"] + st["reflect_rays"] + st["shadow_rays"]) * 3
     assert st["kernel_ms"] > 0 and st["copy_ms"] > 0
+    assert st["timed_launches"] == 1 and st["timed_copies"] == 1  # default: every 64th, first included
     gpu_ctx.reset_stats()
     assert gpu_ctx.stats()["primary_rays"] == 0
+
+
+def test_sampled_timing(gpu_ctx):
+    sc = scenes.config("C1").resized(320, 180)
+    gpu_ctx.set_scene(sc)
+    for every, n, want in [(1, 5, 5), (2, 5, 3), (0, 5, 0), (64, 130, 3)]:
+        gpu_ctx.set_timing(every)
+        gpu_ctx.reset_stats()
+        for _ in range(n):
+            gpu_ctx.render(sc.width, sc.height)
+        st = gpu_ctx.stats()
+        assert st["launches"] == n and st["timed_launches"] == want and st["timed_copies"] == want
+        assert (st["kernel_ms"] > 0) == (want > 0) and st["primary_rays"] == n * sc.width * sc.height
+    with pytest.raises(Exception):
+        gpu_ctx.set_timing(-1)
+    gpu_ctx.set_timing(64)
 
 
 def test_render_async_double_buffered_frames(oracle):

@@ -36,6 +36,9 @@ def main():
         assert lib.rt_set_scene(ctx, S, len(sc.spheres), P, len(sc.planes), L, len(sc.lights),
                                 abi.rt_vec3(*sc.ambient), sc.recursion_limit) == 0
         assert lib.rt_set_camera(ctx, C.byref(sc.c_camera())) == 0
+        if hasattr(lib, "rt_set_timing"):
+            lib.rt_set_timing.argtypes = [C.c_void_p, C.c_int]
+            assert lib.rt_set_timing(ctx, 1) == 0  # time every launch
         libs.append(lib)
         ctxs.append(ctx)
     nl = len(libs)

@@ -1,0 +1,45 @@
+"""Wall-clock per frame of back-to-back rt_render_device calls (bench.py's timed loop
+without the rest), to separate kernel time from per-frame gaps.
+    python tools/frame_wall.py [--config C2] [--frames 400]"""
+import argparse
+import ctypes as C
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "uu-infogr-raytracer_amd"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--frames", type=int, default=400)
+    ap.add_argument("--reps", type=int, default=5)
+    a = ap.parse_args()
+    import torch
+    from raytracer_hip import Context, scenes
+    sc = scenes.config(a.config)
+    W, H = sc.width, sc.height
+    out = torch.empty(W * H, dtype=torch.int32, device="cuda")
+    ctx = Context(1)
+    ctx.set_scene(sc)
+    stream = torch.cuda.current_stream().cuda_stream
+    for _ in range(20):
+        ctx.render_device(W, H, out.data_ptr(), stream)
+    torch.cuda.synchronize()
+    res = []
+    for _ in range(a.reps):
+        t0 = time.perf_counter()
+        for _ in range(a.frames):
+            ctx.render_device(W, H, out.data_ptr(), stream)
+        torch.cuda.synchronize()
+        res.append((time.perf_counter() - t0) / a.frames * 1e6)
+    st = ctx.stats()
+    kern = st["kernel_ms"] / st["launches"] * 1e3 if st["kernel_ms"] else float("nan")
+    print(f"{a.config} {os.environ.get('RT_EXPERIMENT_NO_EVENTS') and 'no-events' or 'events'}: "
+          f"wall/frame min {min(res):.2f} us median {sorted(res)[len(res)//2]:.2f} us; event kernel avg {kern:.2f} us")
+
+
+if __name__ == "__main__":
+    main()

@@ -10,6 +10,7 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <dlfcn.h>
 #include <new>
@@ -84,6 +85,7 @@ struct Device {
     int async_next = 0;
     unsigned long long* d_counters = nullptr;
     std::vector<EventPair> pending, pool;
+    uint64_t op_count[3] = {0, 0, 0};  // operations per timing kind (sampling phase)
     ncclComm_t comm = nullptr;
 };
 
@@ -104,6 +106,8 @@ struct rt_ctx {
     std::string last_error;
     uint64_t frames = 0, pixels = 0, launches = 0;
     double kernel_ms = 0, last_kernel_ms = 0, copy_ms = 0, gather_ms = 0;
+    uint64_t timed[3] = {0, 0, 0};  // timed launches, copies, gathers
+    int timing_every = 64;
     int32_t* host_staging = nullptr;
 };
 
@@ -165,28 +169,35 @@ void drain_events(rt_ctx* ctx, Device& d) {
             } else {
                 ctx->gather_ms += ms;
             }
+            ctx->timed[ep.kind]++;
         }
         d.pool.push_back(ep);
     }
     d.pending.clear();
 }
 
-EventPair* begin_timed(rt_ctx* ctx, Device& d, int kind) {
+// Sampled device timing: the every-th operation of each kind on each device is bracketed
+// by an event pair (rt_set_timing).  Returns whether this one is.
+bool begin_timed(rt_ctx* ctx, Device& d, int kind) {
+    const int every = ctx->timing_every;
+    if (every <= 0 || (d.op_count[kind]++ % (uint64_t)every) != 0) return false;
     if (d.pending.size() >= 4096) drain_events(ctx, d);  // bound host memory; stalls only then
     EventPair ep;
     if (!d.pool.empty()) {
         ep = d.pool.back();
         d.pool.pop_back();
     } else {
-        if (hipEventCreate(&ep.a) != hipSuccess || hipEventCreate(&ep.b) != hipSuccess) return nullptr;
+        if (hipEventCreate(&ep.a) != hipSuccess || hipEventCreate(&ep.b) != hipSuccess) return false;
     }
     ep.kind = kind;
     (void)hipEventRecord(ep.a, d.stream);
     d.pending.push_back(ep);
-    return &d.pending.back();
+    return true;
 }
 
-void end_timed(Device& d) { (void)hipEventRecord(d.pending.back().b, d.stream); }
+void end_timed(Device& d, bool timed) {
+    if (timed) (void)hipEventRecord(d.pending.back().b, d.stream);
+}
 
 // Host-side Vector3 helpers (binary32, no contraction: built with -ffp-contract=off).
 struct H3 {
@@ -271,9 +282,9 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
     lp.out = out;
     hipStream_t saved = d.stream;
     d.stream = stream;
-    begin_timed(ctx, d, 0);
+    const bool timed = begin_timed(ctx, d, 0);
     int e = launch_trace(lp, ctx->layout.generic_pow, stream);
-    end_timed(d);
+    end_timed(d, timed);
     d.stream = saved;
     if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "trace launch failed: %s", hipGetErrorString((hipError_t)e));
     ctx->launches++;
@@ -640,9 +651,10 @@ int rt_render(rt_ctx* ctx, int width, int height, int32_t* pixels) {
             rc = trace_bands(ctx, d, d.stream, width, height, band_rows, g, n, d.d_bands, nullptr);
             if (rc != RT_OK) return rc;
         }
+        std::vector<char> gtimed((size_t)n, 0);
         for (int g = 0; g < n; ++g) {
             DeviceGuard guard(ctx->dev[(size_t)g].id);
-            begin_timed(ctx, ctx->dev[(size_t)g], 2);
+            gtimed[g] = begin_timed(ctx, ctx->dev[(size_t)g], 2);
         }
         if (g_rccl.GroupStart() != 0) return fail(ctx, RT_ERR_RCCL, "ncclGroupStart failed");
         for (int g = 0; g < n; ++g) {
@@ -658,7 +670,7 @@ int rt_render(rt_ctx* ctx, int width, int height, int32_t* pixels) {
         if (g_rccl.GroupEnd() != 0) return fail(ctx, RT_ERR_RCCL, "ncclGroupEnd failed");
         for (int g = 0; g < n; ++g) {
             DeviceGuard guard(ctx->dev[(size_t)g].id);
-            end_timed(ctx->dev[(size_t)g]);
+            end_timed(ctx->dev[(size_t)g], gtimed[g]);
         }
         DeviceGuard guard(d0.id);
         for (int g = 0; g < n; ++g) {
@@ -669,9 +681,9 @@ int rt_render(rt_ctx* ctx, int width, int height, int32_t* pixels) {
         }
     }
     DeviceGuard guard(d0.id);
-    begin_timed(ctx, d0, 1);
+    const bool ctimed = begin_timed(ctx, d0, 1);
     HIP_TRY(ctx, hipMemcpyAsync(pixels, d0.d_frame, frame_bytes, hipMemcpyDeviceToHost, d0.stream));
-    end_timed(d0);
+    end_timed(d0, ctimed);
     HIP_TRY(ctx, hipStreamSynchronize(d0.stream));
     ctx->frames++;
     ctx->pixels += (uint64_t)width * (uint64_t)height;
@@ -693,9 +705,9 @@ int rt_render_async(rt_ctx* ctx, int width, int height, int32_t* pixels) {
     if (rc != RT_OK) return rc;
     rc = trace_bands(ctx, d, d.stream, width, height, height, 0, 1, d.d_frames2[slot], nullptr);
     if (rc != RT_OK) return rc;
-    begin_timed(ctx, d, 1);
+    const bool ctimed = begin_timed(ctx, d, 1);
     HIP_TRY(ctx, hipMemcpyAsync(pixels, d.d_frames2[slot], frame_bytes, hipMemcpyDeviceToHost, d.stream));
-    end_timed(d);
+    end_timed(d, ctimed);
     d.async_next = slot ^ 1;
     ctx->frames++;
     ctx->pixels += (uint64_t)width * (uint64_t)height;
@@ -794,6 +806,17 @@ int rt_get_stats(rt_ctx* ctx, rt_stats* out) {
     out->last_kernel_ms = ctx->last_kernel_ms;
     out->copy_ms = ctx->copy_ms;
     out->gather_ms = ctx->gather_ms;
+    out->timed_launches = ctx->timed[0];
+    out->timed_copies = ctx->timed[1];
+    out->timed_gathers = ctx->timed[2];
+    return RT_OK;
+}
+
+int rt_set_timing(rt_ctx* ctx, int every) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "NULL context");
+    if (every < 0) return fail(ctx, RT_ERR_INVALID_ARG, "rt_set_timing: every must be >= 0");
+    ctx->timing_every = every;
+    for (Device& d : ctx->dev) d.op_count[0] = d.op_count[1] = d.op_count[2] = 0;
     return RT_OK;
 }
 
@@ -807,6 +830,8 @@ int rt_reset_stats(rt_ctx* ctx) {
     }
     ctx->frames = ctx->pixels = ctx->launches = 0;
     ctx->kernel_ms = ctx->last_kernel_ms = ctx->copy_ms = ctx->gather_ms = 0;
+    ctx->timed[0] = ctx->timed[1] = ctx->timed[2] = 0;
+    for (Device& d : ctx->dev) d.op_count[0] = d.op_count[1] = d.op_count[2] = 0;
     return RT_OK;
 }
 

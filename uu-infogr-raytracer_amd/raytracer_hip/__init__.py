@@ -172,6 +172,10 @@ class Context:
     def reset_stats(self):
         self._check(self.lib.rt_reset_stats(self.ptr))
 
+    def set_timing(self, every: int):
+        """Time every `every`-th launch/copy/gather with HIP events (0 = none; default 64)."""
+        self._check(self.lib.rt_set_timing(self.ptr, int(every)))
+
 
 class RayTracer:
     """RayTracer.cs:437-1062, public surface only, rendering on MI355X.

@@ -70,6 +70,7 @@ class rt_stats(C.Structure):
         ("reflect_rays", C.c_uint64), ("shadow_rays", C.c_uint64), ("sphere_tests", C.c_uint64),
         ("plane_tests", C.c_uint64), ("launches", C.c_uint64), ("kernel_ms", C.c_double),
         ("last_kernel_ms", C.c_double), ("copy_ms", C.c_double), ("gather_ms", C.c_double),
+        ("timed_launches", C.c_uint64), ("timed_copies", C.c_uint64), ("timed_gathers", C.c_uint64),
     ]
 
     def as_dict(self):
@@ -102,6 +103,7 @@ EXPORTS = [
     ("rt_wait", C.c_int, [C.c_void_p]),
     ("rt_write_ppm", C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),
     ("rt_debug_segments", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_int)]),
+    ("rt_set_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_get_stats", C.c_int, [C.c_void_p, C.POINTER(rt_stats)]),
     ("rt_reset_stats", C.c_int, [C.c_void_p]),
 ]
@@ -128,7 +130,11 @@ def load_library(path: str | None = None, local: bool = False):
             "(there is no CPU fallback)")
     lib = C.CDLL(p, mode=C.RTLD_LOCAL if local else C.RTLD_GLOBAL)
     for name, res, args in EXPORTS:
-        fn = getattr(lib, name)
+        fn = getattr(lib, name, None)
+        if fn is None:
+            if local:  # an older build under A/B comparison
+                continue
+            raise RuntimeError(f"{p} does not export {name}: stale build, run __graft_entry__.build()")
         fn.restype = res
         fn.argtypes = args
     if path is None:
