@@ -74,3 +74,35 @@ def random_scene(seed: int, width: int = 96, height: int = 64, dense: bool = Fal
         cam_pos = spheres[0].center  # camera inside a sphere
     cam = (cam_pos, float(f32(rng.uniform(-0.6, 0.6))), float(f32(rng.uniform(-0.4, 0.4))))
     return Scene(f"rand{seed}", width, height, spheres, planes, lights, amb, limit, cam)
+
+
+def camera_sweep_scene(seed: int, width: int = 160, height: int = 96) -> Scene:
+    """Views for the per-frame primary screen boxes (view_params): spheres all around the
+    camera, any yaw/pitch, cameras far from the origin, inside or touching spheres, huge and
+    tiny spheres, extreme aspect ratios -- every silhouette must match the oracle."""
+    rng = np.random.default_rng(10_000 + seed)
+    mode = seed % 5
+    cam_pos = _v(rng, -2, 2)
+    if mode == 1:  # far from the origin (direction error of vp - cam grows with |cam|)
+        cam_pos = tuple(float(f32(c * 10.0 ** rng.integers(2, 5))) for c in _v(rng, -1, 1))
+    ns = int(rng.integers(1, 64))
+    spheres = []
+    for k in range(ns):
+        off = rng.normal(size=3)
+        off *= rng.uniform(0.5, 30) / np.linalg.norm(off)
+        r = float(f32(10.0 ** rng.uniform(-2.5, 0.8)))
+        c = tuple(float(f32(cam_pos[j] + off[j])) for j in range(3))
+        if mode == 2 and k == 0:  # camera inside the first sphere
+            c, r = cam_pos, 3.0
+        if mode == 3 and k == 0:  # camera on the first sphere's surface
+            c = (float(f32(cam_pos[0] + 1.0)), cam_pos[1], cam_pos[2])
+            r = 1.0
+        spheres.append(Sphere(c, r, _material(rng)))
+    lights = [Light(_v(rng, -30, 30), float(f32(rng.uniform(0.2, 1.5)))) for _ in range(int(rng.integers(0, 3)))]
+    if mode == 4:
+        width, height = (int(rng.integers(1, 9)), int(rng.integers(40, 200))) if rng.random() < 0.5 else \
+            (int(rng.integers(40, 300)), int(rng.integers(1, 9)))
+    yaw = float(f32(rng.uniform(-7, 7)))
+    pitch = float(f32(rng.uniform(-1.6, 1.6)))
+    limit = int(rng.choice([0, 1, 3]))
+    return Scene(f"sweep{seed}", width, height, spheres, [], lights, (0.1, 0.1, 0.1), limit, (cam_pos, yaw, pitch))

@@ -84,6 +84,17 @@ def test_dense_random_scenes_vs_oracle(gpu_ctx, oracle, seed):
     assert ray_counts(st) == {k: ost[k] for k in ("primary_rays", "reflect_rays", "shadow_rays")}
 
 
+@pytest.mark.parametrize("seed", list(range(200)))
+def test_camera_sweep_vs_oracle(gpu_ctx, oracle, seed):
+    """Primary screen boxes (and both kernels' primary paths) under arbitrary views."""
+    from random_scenes import camera_sweep_scene
+    sc = camera_sweep_scene(seed)
+    want, ost = oracle.render(sc, oracle.MODE_NEAREST, 4)
+    px, st = render_gpu(gpu_ctx, sc)
+    assert_same(px, want, sc.name)
+    assert ray_counts(st) == ray_counts(ost)
+
+
 @pytest.mark.parametrize("w,h", [(1, 1), (17, 13), (15, 16), (16, 15), (33, 65), (1000, 3)])
 def test_ragged_frame_sizes(gpu_ctx, oracle, w, h):
     sc = scenes.config("C3").resized(w, h)

@@ -7,6 +7,8 @@
 // and work counters.  Never throws across the ABI; no CPU fallback.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <climits>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -234,6 +236,59 @@ int bands_of(int H, int band_rows, int first, int step) {
     return first < tb ? (tb - 1 - first) / step + 1 : 0;
 }
 
+// Conservative screen box of a sphere for primary rays (culling only; computed in double).
+//
+// Pixel (x, y) traces the line from the camera along D = R lx + U ly + F lz with
+// lx = (x/W - 0.5) pw, ly = (y/H - 0.5) ph, lz = near (TracePixel :963-971).  By the
+// cull_mask analysis the binary32 IntersectsSphere cannot select the sphere when that line
+// passes at distance >= rho = r (1 + 2^-8) + 2^-8 |u| from its centre (u = C - camera), with
+// |u| also scaled by the kernel's direction error (cancellation in vp - cam, bounded by
+// 2^-20 (|cam| + |D|) / |D|; no box when that exceeds 2^-12).  The distance to the line is at
+// least the distance to the plane through it containing the camera's up (right) axis, so
+// in camera coordinates (cx, cy, cz) the x range follows from the 2-D circle (cx, cz; rho):
+// lx / lz in [tan(phi - g), tan(phi + g)], phi = atan2(cx, cz), g = asin(rho / |(cx, cz)|),
+// valid when cz > rho (sphere strictly in front); same for y with (cy, cz).  Two pixels of
+// slack cover the binary32 pixel-to-direction mapping and the basis' non-orthogonality.
+PrimBox prim_box(const LaunchParams& lp, const DevSphere& s) {
+    const PrimBox all{INT_MIN / 2, INT_MAX / 2, INT_MIN / 2, INT_MAX / 2};
+    const double pw = lp.pw, ph = lp.ph, lz = lp.nearc;
+    if (!(pw > 0) || !(ph > 0) || !(lz > 0) || !std::isfinite(pw) || !std::isfinite(ph) || !std::isfinite(lz))
+        return all;
+    const double cam[3] = {lp.cam[0], lp.cam[1], lp.cam[2]};
+    const double u[3] = {s.cx - cam[0], s.cy - cam[1], s.cz - cam[2]};
+    auto dot3 = [](const double* a, const float* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; };
+    const double ulen = std::sqrt(u[0] * u[0] + u[1] * u[1] + u[2] * u[2]);
+    const double camlen = std::sqrt(cam[0] * cam[0] + cam[1] * cam[1] + cam[2] * cam[2]);
+    const double dmax = std::sqrt(0.25 * pw * pw + 0.25 * ph * ph + lz * lz);
+    const double dir_err = 0x1p-20 * (camlen + dmax) / lz + 0x1p-20;
+    const double r = std::sqrt((double)s.r2);
+    if (!std::isfinite(ulen) || !std::isfinite(r) || !(dir_err <= 0x1p-12)) return all;
+    const double rho = (r * (1.0 + 0x1p-8) + (0x1p-8 + 0x1p-20 + dir_err) * ulen) * (1.0 + 0x1p-16) + 0x1p-60;
+    auto fdot = [](const float* a, const float* b) { return (double)a[0] * b[0] + (double)a[1] * b[1] + (double)a[2] * b[2]; };
+    const double ortho = std::fabs(fdot(lp.right, lp.up)) + std::fabs(fdot(lp.right, lp.fwd)) +
+                         std::fabs(fdot(lp.up, lp.fwd)) + std::fabs(fdot(lp.right, lp.right) - 1.0) +
+                         std::fabs(fdot(lp.up, lp.up) - 1.0) + std::fabs(fdot(lp.fwd, lp.fwd) - 1.0);
+    if (!(ortho < 0x1p-18)) return all;  // the camera basis is orthonormal up to rounding
+    const double cx = dot3(u, lp.right), cy = dot3(u, lp.up), cz = dot3(u, lp.fwd);
+    if (!(cz > rho * (1.0 + 0x1p-10))) return all;
+    auto range = [&](double c, double plane, int n, int& lo, int& hi) {
+        const double phi = std::atan2(c, cz);
+        const double g = std::asin(std::min(1.0, rho / std::sqrt(c * c + cz * cz)));
+        const double tlo = std::tan(phi - g), thi = std::tan(phi + g);
+        const double flo = n * (0.5 + lz * tlo / plane), fhi = n * (0.5 + lz * thi / plane);
+        if (!std::isfinite(flo) || !std::isfinite(fhi)) {
+            lo = INT_MIN / 2, hi = INT_MAX / 2;
+            return;
+        }
+        lo = (int)std::max(-1e9, std::floor(flo) - 2.0);
+        hi = (int)std::min(1e9, std::ceil(fhi) + 2.0);
+    };
+    PrimBox b;
+    range(cx, pw, lp.W, b.x0, b.x1);
+    range(cy, ph, lp.H, b.y0, b.y1);
+    return b;
+}
+
 int view_params(rt_ctx* ctx, int W, int H, LaunchParams& lp) {
     rt_view v;
     int rc = rt_camera_view(&ctx->cam, W, H, &v);
@@ -251,6 +306,7 @@ int view_params(rt_ctx* ctx, int W, int H, LaunchParams& lp) {
         for (size_t i = 0; i < sph.size(); ++i) {
             const H3 oc{lp.cam[0] - sph[i].cx, lp.cam[1] - sph[i].cy, lp.cam[2] - sph[i].cz};
             lp.pc[i] = PrimConst{oc.x, oc.y, oc.z, hdot(oc, oc) - sph[i].r2};
+            lp.pbox[i] = prim_box(lp, sph[i]);
         }
     return RT_OK;
 }

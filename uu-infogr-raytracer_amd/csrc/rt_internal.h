@@ -69,6 +69,12 @@ constexpr int COUNTER_WORDS = COUNTER_SLOTS * 4;
 // every pixel): oc = cam - center and c = Dot(oc, oc) - r^2 of IntersectsSphere
 // (RayTracer.cs:614-619), computed once per frame on the host with the same binary32
 // operations and passed in the kernarg block for up to MAX_PRIM_CONST spheres.
+// Per-frame conservative screen box of sphere i for primary rays: pixels outside
+// [x0, x1] x [y0, y1] cannot select sphere i (view_params in rt_api.cpp derives it).
+struct PrimBox {
+    int x0, x1, y0, y1;
+};
+
 struct PrimConst {
     float ocx, ocy, ocz, c;
 };
@@ -95,8 +101,9 @@ struct LaunchParams {
     int band_rows, band_first, band_step, local_rows;
     int32_t* out;
     unsigned long long* counters;  // COUNTER_SLOTS x {primary, reflect, shadow, pad}
-    int prim_const;                // 1: pc[0..S) valid (S <= MAX_PRIM_CONST)
+    int prim_const;                // 1: pc[0..S) and pbox[0..S) valid (S <= MAX_PRIM_CONST)
     PrimConst pc[MAX_PRIM_CONST];
+    PrimBox pbox[MAX_PRIM_CONST];
 };
 
 // Debug-view segment (layout of rt_segment in include/raytracer_hip.h).

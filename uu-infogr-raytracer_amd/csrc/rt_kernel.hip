@@ -504,8 +504,26 @@ __device__ __forceinline__ f3 shade_direct(const LaunchParams& p, bool is_sphere
     return add(col, mk(m.amb[0], m.amb[1], m.amb[2]));
 }
 
+// Candidate spheres of a wave's primary rays: those whose per-frame screen box (view_params)
+// overlaps the wave's pixels.  Lanes 0 and 63 hold the wave's first and last pixel (the row
+// mapping is monotonic).  Converged call; p.prim_const required.
+#ifndef RT_PRIM_BOX
+#define RT_PRIM_BOX 1
+#endif
+__device__ __forceinline__ unsigned long long prim_box_mask(const LaunchParams& p, int x, int y) {
+    const int x_lo = __builtin_amdgcn_readlane(x, 0), x_hi = __builtin_amdgcn_readlane(x, 63);
+    const int y_lo = __builtin_amdgcn_readlane(y, 0), y_hi = __builtin_amdgcn_readlane(y, 63);
+    const int lane = threadIdx.x & 63;
+    bool cand = false;
+    if (lane < p.S) {
+        const PrimBox b = p.pbox[lane];
+        cand = b.x0 <= x_hi && b.x1 >= x_lo && b.y0 <= y_hi && b.y1 >= y_lo;
+    }
+    return __builtin_amdgcn_ballot_w64(cand);
+}
+
 template <bool PRIMARY, int SMAX>
-__device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d) {
+__device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d, unsigned long long pmask = 0) {
     const float a = dot(d, d);
     const float a2 = 2.0f * a, a4 = 4.0f * a;
     const bool a2_ok = a2 > 0.0f && a2 < __builtin_inff();
@@ -513,7 +531,7 @@ __device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d)
     int win_s = -1;
     if (PRIMARY && p.prim_const) {
         // o == camera: oc = cam - c and c = oc.oc - r^2 are the same per frame (:614-619)
-        for_spheres<SMAX>(p.S, [&](int i) {
+        auto test = [&](int i) {
             const PrimConst pc = p.pc[i];
             const float b = 2.0f * dot(mk(pc.ocx, pc.ocy, pc.ocz), d);
             const float disc = b * b - a4 * pc.c;
@@ -522,7 +540,13 @@ __device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d)
                 best_s = t;
                 win_s = i;
             }
-        });
+        };
+        if constexpr (RT_PRIM_BOX) {
+            // only the wave's candidate spheres, in ascending order (non-candidates give t <= 0)
+            for (unsigned long long m = pmask; m; m &= m - 1) test((int)__builtin_ctzll(m));
+        } else {
+            for_spheres<SMAX>(p.S, test);
+        }
     } else {
         for_spheres<SMAX>(p.S, [&](int i) {
             const float t = sphere_t(o, d, a2, a4, a2_ok, p.sph[i]);
@@ -564,6 +588,7 @@ __global__ __launch_bounds__(256) void trace_direct_kernel(LaunchParams p) {
     const int band = p.band_first + (r / p.band_rows) * p.band_step;
     const int y = band * p.band_rows + (r % p.band_rows);
     const bool valid = x < p.W && r < p.local_rows && y < p.H;
+    const unsigned long long pmask = (RT_PRIM_BOX && p.prim_const) ? prim_box_mask(p, x, y) : 0;
 
     unsigned n_prim = 0, n_refl = 0, n_shadow = 0;
     if (valid) {
@@ -583,7 +608,7 @@ __global__ __launch_bounds__(256) void trace_direct_kernel(LaunchParams p) {
         typename StackFor<K, SCRATCH>::type stk(&ovf);
         stk.origin(d);
         f3 leaf = mk(0.0f, 0.0f, 0.0f);
-        Hit h = nearest_direct<true, SMAX>(p, o, d);
+        Hit h = nearest_direct<true, SMAX>(p, o, d, pmask);
         int count = 0;
         for (;;) {
             if (h.prim == HIT_NONE) break;      // nothing hit: plane colour stays Zero
@@ -868,10 +893,14 @@ __device__ __forceinline__ unsigned long long shadow_cull_mask(const LaunchParam
 // TraceSecondaryRay's asymmetric rule (:804-806, :819-821, :825).
 
 template <bool PRIMARY>
-__device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d, bool active) {
+__device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d, bool active,
+                                              unsigned long long pmask = 0) {
     const unsigned long long am = __builtin_amdgcn_ballot_w64(active);
     if (am == 0) return Hit{0.0f, HIT_NONE};
-    const Bundle B = make_bundle(o, d, active, false);
+    // primary segment: the per-frame screen boxes replace the bundle cull
+    const bool use_box = PRIMARY && RT_PRIM_BOX && p.prim_const;
+    Bundle B{};
+    if (!use_box) B = make_bundle(o, d, active, false);
     if (am != ~0ull) {  // idle lanes trace an exact copy of the first active lane's ray, so
         const int ref = __builtin_ctzll(am);  // they never add divergence (results ignored)
         const f3 ro = readlane3(o, ref), rd = readlane3(d, ref);
@@ -887,7 +916,7 @@ __device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d,
     int win_s = -1;
     for (int base = 0; base < p.S; base += 64) {
         const int n = min(64, p.S - base);
-        unsigned long long m = cull_mask(p, B, base, n);
+        unsigned long long m = use_box ? pmask : cull_mask(p, B, base, n);  // use_box: S <= 64
         while (m) {
             const int i = base + (int)__builtin_ctzll(m);
             m &= m - 1;
@@ -1047,7 +1076,8 @@ __global__ __launch_bounds__(256) void trace_bundle_kernel(LaunchParams p) {
         stk.origin(d);
     f3 leaf = mk(0.0f, 0.0f, 0.0f);
     bool active = valid;
-    Hit h = nearest_bundle<true>(p, o, d, active);
+    const unsigned long long pmask = (RT_PRIM_BOX && p.prim_const) ? prim_box_mask(p, x, y) : 0;
+    Hit h = nearest_bundle<true>(p, o, d, active, pmask);
     for (int count = 0;; ++count) {
         if (active) {
             const bool is_sphere = h.prim >= 0;
@@ -1154,7 +1184,7 @@ __global__ __launch_bounds__(256) void debug_segments_kernel(LaunchParams p, int
                       scale(mk(p.fwd[0], p.fwd[1], p.fwd[2]), 1.0f * p.nearc));
     f3 d = normalize(sub(vp, cam));
     f3 o = cam;
-    Hit h = nearest_direct<true, 0>(p, o, d);
+    Hit h = nearest_direct<true, 0>(p, o, d, p.S >= 64 ? ~0ull : (1ull << p.S) - 1);  // every sphere
     for (int level = 0;; ++level) {
         const bool none = h.prim == HIT_NONE;
         append_segment(out, cap, count, o, add(o, scale(d, none ? 100.0f : h.t)), level == 0 ? 0 : 1,
