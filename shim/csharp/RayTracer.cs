@@ -33,6 +33,13 @@ internal static class Native {
     [DllImport(Lib)] internal static extern int rt_register_host(IntPtr ctx, IntPtr p, UIntPtr bytes);
     [DllImport(Lib)] internal static extern int rt_unregister_host(IntPtr ctx, IntPtr p);
     [DllImport(Lib)] internal static extern int rt_render(IntPtr ctx, int w, int h, IntPtr pixels);
+    // ABI v2 additions (not needed by the synchronous Tick below): pipelined frames, debug view, timing
+    [StructLayout(LayoutKind.Sequential)] internal struct Segment { public Vec3 Origin, End; public int Kind, Pixel; }
+    [DllImport(Lib)] internal static extern int rt_render_async(IntPtr ctx, int w, int h, IntPtr pixels);
+    [DllImport(Lib)] internal static extern int rt_wait(IntPtr ctx);
+    [DllImport(Lib)] internal static extern int rt_debug_segments(IntPtr ctx, int w, int h, int stride,
+                                                                 [Out] Segment[] segments, int capacity, out int count);
+    [DllImport(Lib)] internal static extern int rt_set_timing(IntPtr ctx, int every);
 
     internal static void Check(int rc, IntPtr ctx) {
         if (rc != 0) throw new InvalidOperationException($"libraytracer_hip error {rc}: {Marshal.PtrToStringAnsi(rt_last_error(ctx))}");
