@@ -49,6 +49,7 @@ enum {
  * shades levels 0..L (L+1 stack records).  The reference's own limit is 32
  * (RayTracer.cs:490). */
 #define RT_MAX_RECURSION_LIMIT 63
+#define RT_MAX_LIGHTS 65536  /* per-lane shadow-ray counts are kept in 24 bits */
 
 /* ---- scene description (RayTracer.cs:60-338, :441-469) ---------------------- */
 typedef struct rt_vec3 {

@@ -20,11 +20,17 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--frames", type=int, default=50)
+    ap.add_argument("--strip", default="", help="comma list of spheres,planes,lights,mirrors to remove")
     a = ap.parse_args()
     import torch
     from raytracer_hip import abi, scenes
     torch.cuda.set_device(0)
     sc = scenes.config(a.config)
+    for what in filter(None, a.strip.split(",")):
+        if what == "mirrors":
+            sc.spheres = [x for x in sc.spheres if not any(x.material.km)]
+        else:
+            setattr(sc, what, [])
     W, H = sc.width, sc.height
     out = torch.empty(W * H, dtype=torch.int32, device="cuda")
     ctxs, libs = [], []

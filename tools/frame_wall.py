@@ -16,10 +16,16 @@ def main():
     ap.add_argument("--config", default="C2")
     ap.add_argument("--frames", type=int, default=400)
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--strip", default="", help="comma list of spheres,planes,lights to remove")
+    ap.add_argument("--size", default="", help="WxH override")
     a = ap.parse_args()
     import torch
     from raytracer_hip import Context, scenes
     sc = scenes.config(a.config)
+    for what in filter(None, a.strip.split(",")):
+        setattr(sc, what, [])
+    if a.size:
+        sc = sc.resized(*map(int, a.size.split("x")))
     W, H = sc.width, sc.height
     out = torch.empty(W * H, dtype=torch.int32, device="cuda")
     ctx = Context(1)
@@ -37,7 +43,7 @@ def main():
         res.append((time.perf_counter() - t0) / a.frames * 1e6)
     st = ctx.stats()
     kern = st["kernel_ms"] / st["launches"] * 1e3 if st["kernel_ms"] else float("nan")
-    print(f"{a.config} {os.environ.get('RT_EXPERIMENT_NO_EVENTS') and 'no-events' or 'events'}: "
+    print(f"{a.config} {W}x{H} strip={a.strip or '-'}: "
           f"wall/frame min {min(res):.2f} us median {sorted(res)[len(res)//2]:.2f} us; event kernel avg {kern:.2f} us")
 
 

@@ -462,6 +462,8 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
         (n_lights && !lights))
         return fail(ctx, RT_ERR_INVALID_ARG, "rt_set_scene: bad primitive arrays");
     if (recursion_limit < 0) return fail(ctx, RT_ERR_INVALID_ARG, "recursion_limit must be >= 0");
+    if (n_lights > RT_MAX_LIGHTS)
+        return fail(ctx, RT_ERR_UNSUPPORTED, "n_lights %d > RT_MAX_LIGHTS (%d)", n_lights, RT_MAX_LIGHTS);
     if (recursion_limit > RT_MAX_RECURSION_LIMIT)
         return fail(ctx, RT_ERR_UNSUPPORTED, "recursion_limit %d > RT_MAX_RECURSION_LIMIT (%d)", recursion_limit,
                     RT_MAX_RECURSION_LIMIT);

@@ -229,7 +229,7 @@ struct HybridStack {
     float4 a0, b0, a1, b1;  // top record, second record (separate SSA values: VGPRs)
     HybridOverflow<K>* ov;  // a separate object, so only it is demoted to scratch
     int n = 0;
-    __device__ __forceinline__ explicit HybridStack(HybridOverflow<K>* o) : ov(o) {}
+    __device__ __forceinline__ HybridStack(HybridOverflow<K>* o, float2*, float*) : ov(o) {}
     __device__ __forceinline__ void push(float4 x, float4 y) {
         if (n >= 2) {  // spill the second record
             ov->a[n - 2] = a1;
@@ -258,7 +258,7 @@ struct HybridStack {
 struct NoOverflow {};
 template <int K, bool SCRATCH>
 struct PlainStack : LevelStack<K, SCRATCH> {
-    __device__ __forceinline__ explicit PlainStack(NoOverflow*) {}
+    __device__ __forceinline__ PlainStack(NoOverflow*, float2*, float*) {}
     __device__ __forceinline__ void origin(f3) {}
     __device__ __forceinline__ void pop(const LaunchParams&, float4& x, float4& y) { LevelStack<K, SCRATCH>::pop(x, y); }
 };
@@ -296,7 +296,7 @@ struct CompactStack {
     cvec c;
     f3 d0;
     int n = 0;
-    __device__ __forceinline__ explicit CompactStack(NoOverflow*) {}
+    __device__ __forceinline__ CompactStack(NoOverflow*, float2*, float*) {}
     __device__ __forceinline__ void origin(f3 d) { d0 = d; }
     __device__ __forceinline__ void push(float4 x, float4 y) {
 #pragma unroll
@@ -339,7 +339,7 @@ struct CompactHybridStack {
     int c[K - 2];
     f3 d0;
     int n = 0;
-    __device__ __forceinline__ explicit CompactHybridStack(NoOverflow*) {}
+    __device__ __forceinline__ CompactHybridStack(NoOverflow*, float2*, float*) {}
     __device__ __forceinline__ void origin(f3 d) { d0 = d; }
     __device__ __forceinline__ void push(float4 x, float4 y) {
         if (n >= 2) {
@@ -380,20 +380,64 @@ struct CompactHybridStack {
     }
 };
 
+// RT_STACK 3: the compact levels and the primary direction in LDS, one slot per thread
+// ([level][thread], conflict-free), so they cost no VGPRs; pop re-walks as in CompactStack.
+template <int K>
+struct LdsStack {
+    float2* lv;  // [K][256] (t, primitive code) of this workgroup
+    float* dv;   // [3][256] primary direction
+    int n = 0;
+    __device__ __forceinline__ LdsStack(NoOverflow*, float2* l, float* dd) : lv(l), dv(dd) {}
+    __device__ __forceinline__ void origin(f3 d) {
+        dv[threadIdx.x] = d.x;
+        dv[256 + threadIdx.x] = d.y;
+        dv[512 + threadIdx.x] = d.z;
+    }
+    __device__ __forceinline__ void push(float4 x, float4 y) {
+        lv[n * 256 + threadIdx.x] = make_float2(x.w, y.w);
+        ++n;
+    }
+    __device__ __forceinline__ void pop(const LaunchParams& p, float4& x, float4& y) {
+        --n;
+        f3 o = mk(p.cam[0], p.cam[1], p.cam[2]);
+        f3 d = mk(dv[threadIdx.x], dv[256 + threadIdx.x], dv[512 + threadIdx.x]);
+#pragma unroll 1
+        for (int j = 0; j < K - 1; ++j) {
+            const bool go = j < n;
+            if (__builtin_amdgcn_ballot_w64(go) == 0) break;
+            if (go) {
+                const float2 tc = lv[j * 256 + threadIdx.x];
+                o = reflect_at(p, o, d, tc.x, __float_as_int(tc.y));
+            }
+        }
+        const float2 tk = lv[n * 256 + threadIdx.x];
+        const f3 hp = add(o, scale(d, tk.x));
+        x = make_float4(hp.x, hp.y, hp.z, tk.x);
+        y = make_float4(d.x, d.y, d.z, tk.y);
+    }
+};
+
 #ifndef RT_STACK
-#define RT_STACK 1
+#define RT_STACK 3
 #endif
 template <int K>
 struct MidStack {  // stack for K = 4, 6, 8
-#if RT_STACK == 1
+#if RT_STACK == 3
+    using type = LdsStack<K>;
+    using overflow = NoOverflow;
+    static constexpr int lds_levels = K;
+#elif RT_STACK == 1
     using type = CompactStack<K>;
     using overflow = NoOverflow;
+    static constexpr int lds_levels = 0;
 #elif RT_STACK == 2
     using type = CompactHybridStack<K>;
     using overflow = NoOverflow;
+    static constexpr int lds_levels = 0;
 #else
     using type = HybridStack<K>;
     using overflow = HybridOverflow<K>;
+    static constexpr int lds_levels = 0;
 #endif
 };
 
@@ -402,6 +446,7 @@ template <int K, bool SCRATCH>
 struct StackFor {
     using type = PlainStack<K, SCRATCH>;
     using overflow = NoOverflow;
+    static constexpr int lds_levels = 0;
 };
 template <>
 struct StackFor<4, false> : MidStack<4> {};
@@ -409,6 +454,58 @@ template <>
 struct StackFor<6, false> : MidStack<6> {};
 template <>
 struct StackFor<8, false> : MidStack<8> {};
+
+// Sum of v over the wave (all lanes active): bit-sliced ballots and scalar popcounts, no
+// LDS round trips; the loop runs once per significant bit of the largest v (uniform).
+__device__ __forceinline__ unsigned wave_count(unsigned v) {
+    unsigned s = 0;
+    for (int j = 0; __builtin_amdgcn_ballot_w64(v != 0u) != 0; ++j, v >>= 1)
+        s += (unsigned)__builtin_popcountll(__builtin_amdgcn_ballot_w64((v & 1u) != 0u)) << j;
+    return s;
+}
+
+#ifndef RT_COUNTERS
+#define RT_COUNTERS 2
+#endif
+// Per-lane work counts share one register: reflected segments (<= RT_MAX_RECURSION_LIMIT + 1)
+// in the low byte, shadow rays (<= lights x 64; rt_set_scene caps lights at 65536) above.
+constexpr unsigned CNT_SHADOW_SHIFT = 8;
+constexpr unsigned CNT_REFL_MASK = 0xFFu;
+// Work counters of one wave (converged call, every lane of the workgroup reaches it):
+// RT_COUNTERS 1 = shuffle sums -> LDS -> one workgroup total per spread slot;
+// 2 = ballot/popcount sums, lane 0 adds the wave's totals to slot (wave id % 256).
+__device__ __forceinline__ unsigned wave_sum(unsigned v);
+__device__ __forceinline__ void add_counters(const LaunchParams& p, int lane, int wave, unsigned n_prim,
+                                             unsigned n_refl, unsigned n_shadow) {
+#if RT_COUNTERS == 1
+    __shared__ unsigned red[4][3];
+    n_prim = wave_sum(n_prim);
+    n_refl = wave_sum(n_refl);
+    n_shadow = wave_sum(n_shadow);
+    if (lane == 0) {
+        red[wave][0] = n_prim;
+        red[wave][1] = n_refl;
+        red[wave][2] = n_shadow;
+    }
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const unsigned v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+        const unsigned slot = (blockIdx.y * gridDim.x + blockIdx.x) % COUNTER_SLOTS;
+        if (v) atomicAdd(&p.counters[slot * 4 + threadIdx.x], (unsigned long long)v);
+    }
+#elif RT_COUNTERS == 2
+    const unsigned a = wave_count(n_prim), b = wave_count(n_refl), c = wave_count(n_shadow);
+    if (lane == 0) {
+        const unsigned slot = ((blockIdx.y * gridDim.x + blockIdx.x) * 4u + (unsigned)wave) % COUNTER_SLOTS;
+        unsigned long long* q = &p.counters[slot * 4];
+        if (a) atomicAdd(q + 0, (unsigned long long)a);
+        if (b) atomicAdd(q + 1, (unsigned long long)b);
+        if (c) atomicAdd(q + 2, (unsigned long long)c);
+    }
+#else
+    (void)p, (void)lane, (void)wave, (void)n_prim, (void)n_refl, (void)n_shadow;
+#endif
+}
 
 __device__ __forceinline__ unsigned wave_sum(unsigned v) {
 #pragma unroll
@@ -499,7 +596,7 @@ __device__ __forceinline__ f3 shade_direct(const LaunchParams& p, bool is_sphere
             }
             col = add(col, term);
         }
-        *n_shadow += (unsigned)p.L;
+        *n_shadow += (unsigned)p.L << CNT_SHADOW_SHIFT;
     }
     return add(col, mk(m.amb[0], m.amb[1], m.amb[2]));
 }
@@ -581,6 +678,9 @@ __device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d,
 // DIRECT kernel: each lane walks its own chain with per-lane (divergent) control flow.
 template <int K, bool SCRATCH, bool GPOW, int SMAX>
 __global__ __launch_bounds__(256) void trace_direct_kernel(LaunchParams p) {
+    constexpr int LDS_LEVELS = StackFor<K, SCRATCH>::lds_levels;  // LdsStack slots, else unused
+    __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * 256 : 1];
+    __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * 256 : 1];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
@@ -590,9 +690,8 @@ __global__ __launch_bounds__(256) void trace_direct_kernel(LaunchParams p) {
     const bool valid = x < p.W && r < p.local_rows && y < p.H;
     const unsigned long long pmask = (RT_PRIM_BOX && p.prim_const) ? prim_box_mask(p, x, y) : 0;
 
-    unsigned n_prim = 0, n_refl = 0, n_shadow = 0;
+    unsigned cnt = 0;  // packed: reflected segments (bits 0-7) | shadow rays << CNT_SHADOW_SHIFT
     if (valid) {
-        n_prim = 1;
         const f3 cam = mk(p.cam[0], p.cam[1], p.cam[2]);
         // TracePixel primary ray, :963-971 (no half-pixel offset)
         const float px = (float)x / (float)p.W - 0.5f;
@@ -605,7 +704,7 @@ __global__ __launch_bounds__(256) void trace_direct_kernel(LaunchParams p) {
         f3 o = cam;
 
         typename StackFor<K, SCRATCH>::overflow ovf;
-        typename StackFor<K, SCRATCH>::type stk(&ovf);
+        typename StackFor<K, SCRATCH>::type stk(&ovf, stk_lv, stk_dv);
         stk.origin(d);
         f3 leaf = mk(0.0f, 0.0f, 0.0f);
         Hit h = nearest_direct<true, SMAX>(p, o, d, pmask);
@@ -626,7 +725,7 @@ __global__ __launch_bounds__(256) void trace_direct_kernel(LaunchParams p) {
             if (!(flags & MAT_MIRROR) || RT_ABLATE == 3) break;
             o = reflect_at(p, o, d, h.t, h.prim);  // :854, CalculateReflectionRay :718-720
             ++count;
-            ++n_refl;
+            ++cnt;
             h = nearest_direct<false, SMAX>(p, o, d);
         }
         // backward fold: every recorded hit is shaded in reverse order; a mirror hit
@@ -646,28 +745,13 @@ __global__ __launch_bounds__(256) void trace_direct_kernel(LaunchParams p) {
             const int code = __float_as_int(rb.w);
             const bool is_s = code >= 0;
             col = shade_direct<GPOW, SMAX>(p, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z), ra.w, col,
-                              &n_shadow);
+                              &cnt);
         }
         const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
         p.out[(size_t)r * (size_t)p.W + (size_t)x] = (int32_t)px32;
     }
 
-    // work counters: wave sums -> LDS -> one workgroup total added to a spread slot
-    __shared__ unsigned red[4][3];
-    n_prim = wave_sum(n_prim);
-    n_refl = wave_sum(n_refl);
-    n_shadow = wave_sum(n_shadow);
-    if (lane == 0) {
-        red[wave][0] = n_prim;
-        red[wave][1] = n_refl;
-        red[wave][2] = n_shadow;
-    }
-    __syncthreads();
-    if (threadIdx.x < 3) {
-        const unsigned v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-        const unsigned slot = (blockIdx.y * gridDim.x + blockIdx.x) % COUNTER_SLOTS;
-        if (v) atomicAdd(&p.counters[slot * 4 + threadIdx.x], (unsigned long long)v);
-    }
+    add_counters(p, lane, wave, valid ? 1u : 0u, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1003,7 +1087,7 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
 #endif
             const f3 hs = diff ? hp : B.O;  // idle lanes mirror a shading lane (results ignored)
             bool blocked = !diff;
-            if constexpr (RT_CULLSTATS == 2) *n_shadow += (threadIdx.x & 63) == 0;
+            if constexpr (RT_CULLSTATS == 2) *n_shadow += (unsigned)((threadIdx.x & 63) == 0) << CNT_SHADOW_SHIFT;
             for (int base = 0; RT_ABLATE != 2 && base < p.S; base += 64) {
                 const int n = min(64, p.S - base);
 #if RT_SHADOW_CULL
@@ -1014,7 +1098,7 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
                 while (mk64) {
                     const int i = base + (int)__builtin_ctzll(mk64);
                     mk64 &= mk64 - 1;
-                    if constexpr (RT_CULLSTATS == 1) *n_shadow += (threadIdx.x & 63) == 0;
+                    if constexpr (RT_CULLSTATS == 1) *n_shadow += (unsigned)((threadIdx.x & 63) == 0) << CNT_SHADOW_SHIFT;
                     blocked = blocked | shadow_blocked(hs, l, l_ok, p.sph[i]);  // no short-circuit branch
                     if (__builtin_amdgcn_ballot_w64(!blocked) == 0) break;
                 }
@@ -1039,7 +1123,7 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
             }
             if (diff) col = add(col, term);
         }
-        if (diff && !RT_CULLSTATS) *n_shadow += (unsigned)p.L;
+        if (diff && !RT_CULLSTATS) *n_shadow += (unsigned)p.L << CNT_SHADOW_SHIFT;
     }
     col = add(col, mk(m.amb[0], m.amb[1], m.amb[2]));
     return act ? col : sec;
@@ -1049,6 +1133,9 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
 // every segment and every light can form a wave bundle and cull the sphere list.
 template <int K, bool SCRATCH, bool GPOW>
 __global__ __launch_bounds__(256) void trace_bundle_kernel(LaunchParams p) {
+    constexpr int LDS_LEVELS = StackFor<K, SCRATCH>::lds_levels;  // LdsStack slots, else unused
+    __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * 256 : 1];
+    __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * 256 : 1];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
@@ -1057,7 +1144,7 @@ __global__ __launch_bounds__(256) void trace_bundle_kernel(LaunchParams p) {
     const int y = band * p.band_rows + (r % p.band_rows);
     const bool valid = x < p.W && r < p.local_rows && y < p.H;
 
-    unsigned n_prim = valid ? 1u : 0u, n_refl = 0, n_shadow = 0;
+    unsigned cnt = 0;  // packed: reflected segments (bits 0-7) | shadow rays << CNT_SHADOW_SHIFT
     const f3 cam = mk(p.cam[0], p.cam[1], p.cam[2]);
     // TracePixel primary ray, :963-971 (no half-pixel offset)
     const float px = (float)x / (float)p.W - 0.5f;
@@ -1072,7 +1159,7 @@ __global__ __launch_bounds__(256) void trace_bundle_kernel(LaunchParams p) {
     // forward walk: all lanes advance one segment per iteration (converged loop), each
     // shaded hit pushes a record; mirror hits continue with the reflected segment
     typename StackFor<K, SCRATCH>::overflow ovf;
-    typename StackFor<K, SCRATCH>::type stk(&ovf);
+    typename StackFor<K, SCRATCH>::type stk(&ovf, stk_lv, stk_dv);
         stk.origin(d);
     f3 leaf = mk(0.0f, 0.0f, 0.0f);
     bool active = valid;
@@ -1095,7 +1182,7 @@ __global__ __launch_bounds__(256) void trace_bundle_kernel(LaunchParams p) {
                     active = false;
                 } else {
                     o = reflect_at(p, o, d, h.t, h.prim);  // :854, CalculateReflectionRay :718-720
-                    ++n_refl;
+                    ++cnt;
                 }
             }
         }
@@ -1136,29 +1223,14 @@ __global__ __launch_bounds__(256) void trace_bundle_kernel(LaunchParams p) {
         const int code = __float_as_int(rb.w);
         const bool is_s = code >= 0;
         col = shade_bundle<GPOW>(p, act, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z), ra.w, col,
-                          &n_shadow);
+                          &cnt);
     }
     if (valid) {
         const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
         p.out[(size_t)r * (size_t)p.W + (size_t)x] = (int32_t)px32;
     }
 
-    // work counters: wave sums -> LDS -> one workgroup total added to a spread slot
-    __shared__ unsigned red[4][3];
-    n_prim = wave_sum(n_prim);
-    n_refl = wave_sum(n_refl);
-    n_shadow = wave_sum(n_shadow);
-    if (lane == 0) {
-        red[wave][0] = n_prim;
-        red[wave][1] = n_refl;
-        red[wave][2] = n_shadow;
-    }
-    __syncthreads();
-    if (threadIdx.x < 3) {
-        const unsigned v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
-        const unsigned slot = (blockIdx.y * gridDim.x + blockIdx.x) % COUNTER_SLOTS;
-        if (v) atomicAdd(&p.counters[slot * 4 + threadIdx.x], (unsigned long long)v);
-    }
+    add_counters(p, lane, wave, valid ? 1u : 0u, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT);
 }
 
 // ---------------------------------------------------------------------------------

@@ -22,6 +22,7 @@ RT_ERR_UNSUPPORTED = -5
 RT_ERR_RCCL = -6
 RT_ERR_OOM = -7
 RT_MAX_RECURSION_LIMIT = 63
+RT_MAX_LIGHTS = 65536
 
 RT_KEY_W, RT_KEY_A, RT_KEY_S, RT_KEY_D, RT_KEY_SPACE, RT_KEY_SHIFT = 1, 2, 3, 4, 5, 6
 
