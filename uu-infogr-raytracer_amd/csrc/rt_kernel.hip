@@ -4,8 +4,9 @@
 // *PhongShading :652-708 -> TraceSecondaryRay :789-826 -> ShiftColor :1046-1052).
 //
 // Design (MI355X-first, not a translation of the C# recursion):
-//  * one wave64 lane per pixel; a wave covers an 8x8 pixel tile, a 256-thread workgroup
-//    a 16x16 tile (ray coherence -> fewer divergent primitive hits per wave);
+//  * one wave64 lane per pixel; a wave covers an 8x8 pixel tile (ray coherence -> fewer
+//    divergent primitive hits per wave) and is its own workgroup (A/B: 2x2-wave groups
+//    +8 % on C4, where a group's LDS stack slots were held until its slowest wave ended);
 //  * the scene is tiny (< 6 KB at 64 spheres) and every loop over spheres / planes / lights
 //    is wave-uniform, so primitive data is read with scalar loads (SGPR operands); the
 //    camera-relative sphere constants of the primary segment come in the kernarg block;
@@ -31,6 +32,18 @@
 #endif
 // RT_CULLSTATS (experiments only): the bundle kernel's reflect/shadow counters count the
 // wave-iterations of its shadow exact-test loops (1) or its shadow bundles (2) instead of rays.
+// Workgroup shape of the trace kernels: WG_WX x WG_WY waves, each an 8x8 pixel tile.
+// A/B (C2/C3/C4): 1x1 1.00/1.00/0.92, 2x1 0.99/1.00/0.95, 2x2 = 1, 4x2 1.04/1.03/1.13,
+// 4x4 1.10/1.14/1.29 (kernel time relative to 2x2).
+#ifndef RT_WG_WX
+#define RT_WG_WX 1
+#endif
+#ifndef RT_WG_WY
+#define RT_WG_WY 1
+#endif
+constexpr int WG_WX = RT_WG_WX, WG_WY = RT_WG_WY, WG_WAVES = WG_WX * WG_WY, WG_THREADS = 64 * WG_WAVES;
+constexpr int TILE_W = 8 * WG_WX, TILE_H = 8 * WG_WY;
+
 #ifndef RT_CULLSTATS
 #define RT_CULLSTATS 0
 #endif
@@ -384,33 +397,33 @@ struct CompactHybridStack {
 // ([level][thread], conflict-free), so they cost no VGPRs; pop re-walks as in CompactStack.
 template <int K>
 struct LdsStack {
-    float2* lv;  // [K][256] (t, primitive code) of this workgroup
-    float* dv;   // [3][256] primary direction
+    float2* lv;  // [K][WG_THREADS] (t, primitive code) of this workgroup
+    float* dv;   // [3][WG_THREADS] primary direction
     int n = 0;
     __device__ __forceinline__ LdsStack(NoOverflow*, float2* l, float* dd) : lv(l), dv(dd) {}
     __device__ __forceinline__ void origin(f3 d) {
         dv[threadIdx.x] = d.x;
-        dv[256 + threadIdx.x] = d.y;
-        dv[512 + threadIdx.x] = d.z;
+        dv[WG_THREADS + threadIdx.x] = d.y;
+        dv[2 * WG_THREADS + threadIdx.x] = d.z;
     }
     __device__ __forceinline__ void push(float4 x, float4 y) {
-        lv[n * 256 + threadIdx.x] = make_float2(x.w, y.w);
+        lv[n * WG_THREADS + threadIdx.x] = make_float2(x.w, y.w);
         ++n;
     }
     __device__ __forceinline__ void pop(const LaunchParams& p, float4& x, float4& y) {
         --n;
         f3 o = mk(p.cam[0], p.cam[1], p.cam[2]);
-        f3 d = mk(dv[threadIdx.x], dv[256 + threadIdx.x], dv[512 + threadIdx.x]);
+        f3 d = mk(dv[threadIdx.x], dv[WG_THREADS + threadIdx.x], dv[2 * WG_THREADS + threadIdx.x]);
 #pragma unroll 1
         for (int j = 0; j < K - 1; ++j) {
             const bool go = j < n;
             if (__builtin_amdgcn_ballot_w64(go) == 0) break;
             if (go) {
-                const float2 tc = lv[j * 256 + threadIdx.x];
+                const float2 tc = lv[j * WG_THREADS + threadIdx.x];
                 o = reflect_at(p, o, d, tc.x, __float_as_int(tc.y));
             }
         }
-        const float2 tk = lv[n * 256 + threadIdx.x];
+        const float2 tk = lv[n * WG_THREADS + threadIdx.x];
         const f3 hp = add(o, scale(d, tk.x));
         x = make_float4(hp.x, hp.y, hp.z, tk.x);
         y = make_float4(d.x, d.y, d.z, tk.y);
@@ -478,7 +491,7 @@ __device__ __forceinline__ unsigned wave_sum(unsigned v);
 __device__ __forceinline__ void add_counters(const LaunchParams& p, int lane, int wave, unsigned n_prim,
                                              unsigned n_refl, unsigned n_shadow) {
 #if RT_COUNTERS == 1
-    __shared__ unsigned red[4][3];
+    __shared__ unsigned red[WG_WAVES][3];
     n_prim = wave_sum(n_prim);
     n_refl = wave_sum(n_refl);
     n_shadow = wave_sum(n_shadow);
@@ -489,14 +502,15 @@ __device__ __forceinline__ void add_counters(const LaunchParams& p, int lane, in
     }
     __syncthreads();
     if (threadIdx.x < 3) {
-        const unsigned v = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x];
+        unsigned v = 0;
+        for (int w = 0; w < WG_WAVES; ++w) v += red[w][threadIdx.x];
         const unsigned slot = (blockIdx.y * gridDim.x + blockIdx.x) % COUNTER_SLOTS;
         if (v) atomicAdd(&p.counters[slot * 4 + threadIdx.x], (unsigned long long)v);
     }
 #elif RT_COUNTERS == 2
     const unsigned a = wave_count(n_prim), b = wave_count(n_refl), c = wave_count(n_shadow);
     if (lane == 0) {
-        const unsigned slot = ((blockIdx.y * gridDim.x + blockIdx.x) * 4u + (unsigned)wave) % COUNTER_SLOTS;
+        const unsigned slot = ((blockIdx.y * gridDim.x + blockIdx.x) * (unsigned)WG_WAVES + (unsigned)wave) % COUNTER_SLOTS;
         unsigned long long* q = &p.counters[slot * 4];
         if (a) atomicAdd(q + 0, (unsigned long long)a);
         if (b) atomicAdd(q + 1, (unsigned long long)b);
@@ -677,14 +691,14 @@ __device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d,
 
 // DIRECT kernel: each lane walks its own chain with per-lane (divergent) control flow.
 template <int K, bool SCRATCH, bool GPOW, int SMAX>
-__global__ __launch_bounds__(256) void trace_direct_kernel(LaunchParams p) {
+__global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p) {
     constexpr int LDS_LEVELS = StackFor<K, SCRATCH>::lds_levels;  // LdsStack slots, else unused
-    __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * 256 : 1];
-    __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * 256 : 1];
+    __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
+    __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * WG_THREADS : 1];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int r = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const int x = blockIdx.x * TILE_W + (wave % WG_WX) * 8 + (lane & 7);
+    const int r = blockIdx.y * TILE_H + (wave / WG_WX) * 8 + (lane >> 3);
     const int band = p.band_first + (r / p.band_rows) * p.band_step;
     const int y = band * p.band_rows + (r % p.band_rows);
     const bool valid = x < p.W && r < p.local_rows && y < p.H;
@@ -1132,14 +1146,14 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
 // BUNDLE kernel (scenes with >= CULL_MIN_SPHERES spheres): converged control flow so that
 // every segment and every light can form a wave bundle and cull the sphere list.
 template <int K, bool SCRATCH, bool GPOW>
-__global__ __launch_bounds__(256) void trace_bundle_kernel(LaunchParams p) {
+__global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel(LaunchParams p) {
     constexpr int LDS_LEVELS = StackFor<K, SCRATCH>::lds_levels;  // LdsStack slots, else unused
-    __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * 256 : 1];
-    __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * 256 : 1];
+    __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
+    __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * WG_THREADS : 1];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int x = blockIdx.x * 16 + (wave & 1) * 8 + (lane & 7);
-    const int r = blockIdx.y * 16 + (wave >> 1) * 8 + (lane >> 3);
+    const int x = blockIdx.x * TILE_W + (wave % WG_WX) * 8 + (lane & 7);
+    const int r = blockIdx.y * TILE_H + (wave / WG_WX) * 8 + (lane >> 3);
     const int band = p.band_first + (r / p.band_rows) * p.band_step;
     const int y = band * p.band_rows + (r % p.band_rows);
     const bool valid = x < p.W && r < p.local_rows && y < p.H;
@@ -1330,8 +1344,8 @@ RT_DEFINE_DISPATCH(launch_bundle, trace_bundle_kernel)
 
 int launch_trace(const LaunchParams& p, bool generic_pow, void* stream) {
     if (p.local_rows <= 0 || p.W <= 0) return (int)hipSuccess;
-    const dim3 grid((unsigned)((p.W + 15) / 16), (unsigned)((p.local_rows + 15) / 16));
-    const dim3 block(256);
+    const dim3 grid((unsigned)((p.W + TILE_W - 1) / TILE_W), (unsigned)((p.local_rows + TILE_H - 1) / TILE_H));
+    const dim3 block(WG_THREADS);
     hipStream_t s = (hipStream_t)stream;
     // bundle culling pays for its per-wave bounds only with enough spheres (A/B: +15 % at
     // 8 spheres, 3x faster at 64)
