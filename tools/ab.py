@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--frames", type=int, default=50)
     ap.add_argument("--strip", default="", help="comma list of spheres,planes,lights,mirrors to remove")
+    ap.add_argument("--limit", type=int, default=None, help="override the recursion limit")
     a = ap.parse_args()
     import torch
     from raytracer_hip import abi, scenes
@@ -31,6 +32,8 @@ def main():
             sc.spheres = [x for x in sc.spheres if not any(x.material.km)]
         else:
             setattr(sc, what, [])
+    if a.limit is not None:
+        sc.recursion_limit = a.limit
     W, H = sc.width, sc.height
     out = torch.empty(W * H, dtype=torch.int32, device="cuda")
     ctxs, libs = [], []

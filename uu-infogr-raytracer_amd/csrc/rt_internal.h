@@ -81,7 +81,10 @@ struct PrimConst {
 constexpr int MAX_PRIM_CONST = 64;
 
 // Scenes with at least this many spheres use wave-bundle culling (rt_kernel.hip).
-constexpr int CULL_MIN_SPHERES = 12;
+#ifndef RT_CULL_MIN
+#define RT_CULL_MIN 12
+#endif
+constexpr int CULL_MIN_SPHERES = RT_CULL_MIN;
 
 
 // Per-launch parameters (passed by value as the kernel argument block, < 4 KiB).

@@ -461,6 +461,15 @@ struct StackFor {
     using overflow = NoOverflow;
     static constexpr int lds_levels = 0;
 };
+#ifndef RT_LDS_SMALL
+#define RT_LDS_SMALL 1
+#endif
+#if RT_STACK == 3 && RT_LDS_SMALL
+template <>
+struct StackFor<1, false> : MidStack<1> {};
+template <>
+struct StackFor<2, false> : MidStack<2> {};
+#endif
 template <>
 struct StackFor<4, false> : MidStack<4> {};
 template <>
