@@ -99,10 +99,22 @@ def camera_sweep_scene(seed: int, width: int = 160, height: int = 96) -> Scene:
             r = 1.0
         spheres.append(Sphere(c, r, _material(rng)))
     lights = [Light(_v(rng, -30, 30), float(f32(rng.uniform(0.2, 1.5)))) for _ in range(int(rng.integers(0, 3)))]
+    planes = []
+    if seed % 2 == 0:  # mirror planes: first reflections use the per-frame mirror boxes
+        for _ in range(int(rng.integers(1, 4))):
+            v = rng.normal(size=3)
+            v = v / np.linalg.norm(v)
+            n = tuple(float(f32(x)) for x in v)
+            off = rng.normal(size=3)
+            off *= rng.uniform(0.5, 12) / np.linalg.norm(off)
+            c = tuple(float(f32(cam_pos[j] + off[j])) for j in range(3))
+            km = _v(rng, 0.3, 1.0)
+            mat = Material.mirror(km) if rng.random() < 0.5 else Material.diffuse_mirror(_color(rng), km)
+            planes.append(Plane(c, n, mat))
     if mode == 4:
         width, height = (int(rng.integers(1, 9)), int(rng.integers(40, 200))) if rng.random() < 0.5 else \
             (int(rng.integers(40, 300)), int(rng.integers(1, 9)))
     yaw = float(f32(rng.uniform(-7, 7)))
     pitch = float(f32(rng.uniform(-1.6, 1.6)))
     limit = int(rng.choice([0, 1, 3]))
-    return Scene(f"sweep{seed}", width, height, spheres, [], lights, (0.1, 0.1, 0.1), limit, (cam_pos, yaw, pitch))
+    return Scene(f"sweep{seed}", width, height, spheres, planes, lights, (0.1, 0.1, 0.1), limit, (cam_pos, yaw, pitch))
