@@ -329,3 +329,40 @@ def test_debug_tick_composites_inset_over_exact_frame(oracle):
     colours = set(np.unique(img[inset]).tolist())
     assert colours <= {0, debugview.CIRCLE_COLOR, *debugview.KIND_COLORS.values()}
     assert colours & set(debugview.KIND_COLORS.values())
+
+
+def test_set_scene_waits_for_frames_in_flight(gpu_ctx, golden):
+    """rt_set_scene right after rt_render_device on a caller stream (no host sync): the
+    in-flight frame must still see the old scene (the upload waits for the device)."""
+    import torch
+    a, b = golden["cases"]["C3_96x54"], golden["cases"]["C1_64"]
+    sa, sb = scenes.config(a["config"]).resized(a["width"], a["height"]), scenes.config(b["config"]).resized(
+        b["width"], b["height"])
+    outs = []
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        for k in range(6):
+            sc = sa if k % 2 == 0 else sb
+            gpu_ctx.set_scene(sc)
+            out = torch.empty(sc.width * sc.height, dtype=torch.int32, device="cuda")
+            gpu_ctx.render_device(sc.width, sc.height, out.data_ptr(), s.cuda_stream)
+            outs.append(out)
+    s.synchronize()
+    for k, out in enumerate(outs):
+        e = a if k % 2 == 0 else b
+        assert crc(out.cpu().numpy()) == e["crc32"], k
+
+
+def test_two_frames_in_flight_on_two_streams(gpu_ctx, golden):
+    """bench.py's swap chain: frames alternate between two streams and buffers."""
+    import torch
+    e = golden["cases"]["C2_96x54"]
+    sc = scenes.config(e["config"]).resized(e["width"], e["height"])
+    gpu_ctx.set_scene(sc)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    outs = [torch.full((sc.width * sc.height,), -1, dtype=torch.int32, device="cuda") for _ in range(2)]
+    torch.cuda.synchronize()
+    for k in range(10):
+        gpu_ctx.render_device(sc.width, sc.height, outs[k % 2].data_ptr(), streams[k % 2].cuda_stream)
+    torch.cuda.synchronize()
+    assert all(crc(o.cpu().numpy()) == e["crc32"] for o in outs)

@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--strip", default="", help="comma list of spheres,planes,lights to remove")
     ap.add_argument("--size", default="", help="WxH override")
+    ap.add_argument("--inflight", type=int, default=1, help="frames in flight (streams/buffers)")
     a = ap.parse_args()
     import torch
     from raytracer_hip import Context, scenes
@@ -27,23 +28,24 @@ def main():
     if a.size:
         sc = sc.resized(*map(int, a.size.split("x")))
     W, H = sc.width, sc.height
-    out = torch.empty(W * H, dtype=torch.int32, device="cuda")
+    outs = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in range(a.inflight)]
     ctx = Context(1)
     ctx.set_scene(sc)
-    stream = torch.cuda.current_stream().cuda_stream
-    for _ in range(20):
-        ctx.render_device(W, H, out.data_ptr(), stream)
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(a.inflight - 1)]
+    sp = [s.cuda_stream for s in streams]
+    for k in range(20):
+        ctx.render_device(W, H, outs[k % a.inflight].data_ptr(), sp[k % a.inflight])
     torch.cuda.synchronize()
     res = []
     for _ in range(a.reps):
         t0 = time.perf_counter()
-        for _ in range(a.frames):
-            ctx.render_device(W, H, out.data_ptr(), stream)
+        for k in range(a.frames):
+            ctx.render_device(W, H, outs[k % a.inflight].data_ptr(), sp[k % a.inflight])
         torch.cuda.synchronize()
         res.append((time.perf_counter() - t0) / a.frames * 1e6)
     st = ctx.stats()
     kern = st["kernel_ms"] / st["launches"] * 1e3 if st["kernel_ms"] else float("nan")
-    print(f"{a.config} {W}x{H} strip={a.strip or '-'}: "
+    print(f"{a.config} {W}x{H} strip={a.strip or '-'} inflight={a.inflight}: "
           f"wall/frame min {min(res):.2f} us median {sorted(res)[len(res)//2]:.2f} us; event kernel avg {kern:.2f} us")
 
 

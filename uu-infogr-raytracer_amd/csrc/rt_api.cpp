@@ -84,6 +84,7 @@ struct Device {
     size_t gather_cap = 0;
     int32_t* d_frames2[2] = {nullptr, nullptr};  // rt_render_async double buffer
     size_t frames2_cap[2] = {0, 0};
+    hipStream_t slot_stream[2] = {nullptr, nullptr};  // one per buffer: two frames in flight
     int async_next = 0;
     unsigned long long* d_counters = nullptr;
     std::vector<EventPair> pending, pool;
@@ -439,7 +440,7 @@ void rt_destroy(rt_ctx* ctx) {
     if (!ctx) return;
     for (Device& d : ctx->dev) {
         DeviceGuard guard(d.id);
-        if (d.stream) (void)hipStreamSynchronize(d.stream);
+        (void)hipDeviceSynchronize();  // kernels on caller streams may still read our buffers
         for (EventPair& ep : d.pending) (void)hipEventDestroy(ep.a), (void)hipEventDestroy(ep.b);
         for (EventPair& ep : d.pool) (void)hipEventDestroy(ep.a), (void)hipEventDestroy(ep.b);
         if (d.comm && g_rccl.CommDestroy) (void)g_rccl.CommDestroy(d.comm);
@@ -450,6 +451,8 @@ void rt_destroy(rt_ctx* ctx) {
         for (int i = 0; i < 2; ++i)
             if (d.d_frames2[i]) (void)hipFree(d.d_frames2[i]);
         if (d.d_counters) (void)hipFree(d.d_counters);
+        for (hipStream_t s : d.slot_stream)
+            if (s) (void)hipStreamDestroy(s);
         if (d.stream) (void)hipStreamDestroy(d.stream);
     }
     delete ctx;
@@ -536,7 +539,9 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
         if ((mat[i].flags & MAT_SPEC) && mat[i].pow_kind == POW_GENERIC) L.generic_pow = true;
     for (Device& d : ctx->dev) {
         DeviceGuard guard(d.id);
-        HIP_TRY(ctx, hipStreamSynchronize(d.stream));
+        // frames in flight on any stream (rt_render_device callers', the async slots) read
+        // the scene being replaced
+        HIP_TRY(ctx, hipDeviceSynchronize());
         int rc = grow(ctx, &d.d_scene, &d.scene_cap, L.bytes);
         if (rc != RT_OK) return rc;
         HIP_TRY(ctx, hipMemcpy(d.d_scene, blob.data(), L.bytes, hipMemcpyHostToDevice));
@@ -759,13 +764,20 @@ int rt_render_async(rt_ctx* ctx, int width, int height, int32_t* pixels) {
     DeviceGuard guard(d.id);
     const size_t frame_bytes = (size_t)width * height * sizeof(int32_t);
     const int slot = d.async_next;
+    if (!d.slot_stream[slot]) HIP_TRY(ctx, hipStreamCreateWithFlags(&d.slot_stream[slot], hipStreamNonBlocking));
+    hipStream_t s = d.slot_stream[slot];
     rc = grow(ctx, (void**)&d.d_frames2[slot], &d.frames2_cap[slot], frame_bytes);
     if (rc != RT_OK) return rc;
-    rc = trace_bands(ctx, d, d.stream, width, height, height, 0, 1, d.d_frames2[slot], nullptr);
+    // frame k on slot k % 2: its trace overlaps the tail of frame k-1's trace and its D2H
+    rc = trace_bands(ctx, d, s, width, height, height, 0, 1, d.d_frames2[slot], nullptr);
     if (rc != RT_OK) return rc;
+    hipStream_t saved = d.stream;
+    d.stream = s;  // time the copy on the stream it runs on
     const bool ctimed = begin_timed(ctx, d, 1);
-    HIP_TRY(ctx, hipMemcpyAsync(pixels, d.d_frames2[slot], frame_bytes, hipMemcpyDeviceToHost, d.stream));
+    hipError_t e = hipMemcpyAsync(pixels, d.d_frames2[slot], frame_bytes, hipMemcpyDeviceToHost, s);
     end_timed(d, ctimed);
+    d.stream = saved;
+    if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "rt_render_async: %s", hipGetErrorString(e));
     d.async_next = slot ^ 1;
     ctx->frames++;
     ctx->pixels += (uint64_t)width * (uint64_t)height;
@@ -777,6 +789,8 @@ int rt_wait(rt_ctx* ctx) {
     for (Device& d : ctx->dev) {
         DeviceGuard guard(d.id);
         HIP_TRY(ctx, hipStreamSynchronize(d.stream));
+        for (hipStream_t st : d.slot_stream)
+            if (st) HIP_TRY(ctx, hipStreamSynchronize(st));
     }
     return RT_OK;
 }
