@@ -406,6 +406,7 @@ int rt_create(int n_gpus, rt_ctx** out_ctx) {
         hipError_t e = hipStreamCreateWithFlags(&d.stream, hipStreamNonBlocking);
         if (e == hipSuccess) e = hipMalloc((void**)&d.d_counters, COUNTER_WORDS * sizeof(unsigned long long));
         if (e == hipSuccess) e = hipMemset(d.d_counters, 0, COUNTER_WORDS * sizeof(unsigned long long));
+        if (e == hipSuccess) e = hipDeviceSynchronize();  // kernels run on non-blocking streams
         if (e != hipSuccess) {
             int rc = fail(ctx, RT_ERR_HIP, "device %d init: %s", d.id, hipGetErrorString(e));
             g_last_error = ctx->last_error;
@@ -814,7 +815,7 @@ int rt_debug_segments(rt_ctx* ctx, int width, int height, int sample_stride, rt_
     DevSegment* d_out = nullptr;
     unsigned* d_count = nullptr;
     HIP_TRY(ctx, hipMalloc((void**)&d_count, sizeof(unsigned)));
-    hipError_t e = hipMemset(d_count, 0, sizeof(unsigned));
+    hipError_t e = hipMemsetAsync(d_count, 0, sizeof(unsigned), d.stream);  // same stream as the kernel
     if (e == hipSuccess && capacity > 0) e = hipMalloc((void**)&d_out, sizeof(DevSegment) * (size_t)capacity);
     if (e == hipSuccess) e = (hipError_t)launch_debug_segments(lp, sample_stride, d_out, capacity, d_count, d.stream);
     unsigned n = 0;
@@ -899,6 +900,7 @@ int rt_reset_stats(rt_ctx* ctx) {
         HIP_TRY(ctx, hipDeviceSynchronize());
         drain_events(ctx, d);
         HIP_TRY(ctx, hipMemset(d.d_counters, 0, COUNTER_WORDS * sizeof(unsigned long long)));
+        HIP_TRY(ctx, hipDeviceSynchronize());  // the clear lands before the next frame's atomics
     }
     ctx->frames = ctx->pixels = ctx->launches = 0;
     ctx->kernel_ms = ctx->last_kernel_ms = ctx->copy_ms = ctx->gather_ms = 0;

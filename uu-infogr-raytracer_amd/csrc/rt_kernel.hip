@@ -42,7 +42,7 @@
 #define RT_WG_WY 1
 #endif
 constexpr int WG_WX = RT_WG_WX, WG_WY = RT_WG_WY, WG_WAVES = WG_WX * WG_WY, WG_THREADS = 64 * WG_WAVES;
-constexpr int TILE_W = 8 * WG_WX, TILE_H = 8 * WG_WY;
+[[maybe_unused]] constexpr int TILE_W = 8 * WG_WX, TILE_H = 8 * WG_WY;
 
 #ifndef RT_CULLSTATS
 #define RT_CULLSTATS 0
