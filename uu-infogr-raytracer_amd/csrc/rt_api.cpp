@@ -108,6 +108,7 @@ struct rt_ctx {
     rt_camera cam{};
     std::string last_error;
     uint64_t frames = 0, pixels = 0, launches = 0;
+    uint64_t prim_rays = 0;  // traced pixels (the kernels count only reflect/shadow rays)
     double kernel_ms = 0, last_kernel_ms = 0, copy_ms = 0, gather_ms = 0;
     uint64_t timed[3] = {0, 0, 0};  // timed launches, copies, gathers
     int timing_every = 64;
@@ -345,6 +346,10 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
     d.stream = saved;
     if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "trace launch failed: %s", hipGetErrorString((hipError_t)e));
     ctx->launches++;
+    for (int k = 0; k < nb; ++k) {  // pixels of rows < H in the launched bands
+        const long long y0 = (long long)(first + k * step) * band_rows;
+        ctx->prim_rays += (uint64_t)std::min<long long>(band_rows, (long long)H - y0) * (uint64_t)W;
+    }
     return RT_OK;
 }
 
@@ -868,12 +873,12 @@ int rt_get_stats(rt_ctx* ctx, rt_stats* out) {
     }
     out->frames = ctx->frames;
     out->pixels = ctx->pixels;
-    out->primary_rays = c[0];
+    out->primary_rays = ctx->prim_rays;
     out->reflect_rays = c[1];
     out->shadow_rays = c[2];
     const uint64_t S = (uint64_t)ctx->layout.S, P = (uint64_t)ctx->layout.P;
-    out->sphere_tests = (c[0] + c[1] + c[2]) * S;
-    out->plane_tests = (c[0] + c[1]) * P;
+    out->sphere_tests = (ctx->prim_rays + c[1] + c[2]) * S;
+    out->plane_tests = (ctx->prim_rays + c[1]) * P;
     out->launches = ctx->launches;
     out->kernel_ms = ctx->kernel_ms;
     out->last_kernel_ms = ctx->last_kernel_ms;
@@ -902,7 +907,7 @@ int rt_reset_stats(rt_ctx* ctx) {
         HIP_TRY(ctx, hipMemset(d.d_counters, 0, COUNTER_WORDS * sizeof(unsigned long long)));
         HIP_TRY(ctx, hipDeviceSynchronize());  // the clear lands before the next frame's atomics
     }
-    ctx->frames = ctx->pixels = ctx->launches = 0;
+    ctx->frames = ctx->pixels = ctx->launches = ctx->prim_rays = 0;
     ctx->kernel_ms = ctx->last_kernel_ms = ctx->copy_ms = ctx->gather_ms = 0;
     ctx->timed[0] = ctx->timed[1] = ctx->timed[2] = 0;
     for (Device& d : ctx->dev) d.op_count[0] = d.op_count[1] = d.op_count[2] = 0;

@@ -495,7 +495,8 @@ constexpr unsigned CNT_SHADOW_SHIFT = 8;
 constexpr unsigned CNT_REFL_MASK = 0xFFu;
 // Work counters of one wave (converged call, every lane of the workgroup reaches it):
 // RT_COUNTERS 1 = shuffle sums -> LDS -> one workgroup total per spread slot;
-// 2 = ballot/popcount sums, lane 0 adds the wave's totals to slot (wave id % 256).
+// 2 = ballot/popcount sums, lane 0 adds the wave's reflect/shadow totals to slot
+// (wave id % 256); primary rays are the traced pixels, counted on the host.
 __device__ __forceinline__ unsigned wave_sum(unsigned v);
 __device__ __forceinline__ void add_counters(const LaunchParams& p, int lane, int wave, unsigned n_prim,
                                              unsigned n_refl, unsigned n_shadow) {
@@ -517,11 +518,13 @@ __device__ __forceinline__ void add_counters(const LaunchParams& p, int lane, in
         if (v) atomicAdd(&p.counters[slot * 4 + threadIdx.x], (unsigned long long)v);
     }
 #elif RT_COUNTERS == 2
-    const unsigned a = wave_count(n_prim), b = wave_count(n_refl), c = wave_count(n_shadow);
+    // primary rays = traced pixels, counted on the host (every atomic is a memory round trip
+    // on MI355X: 32 B of HBM write traffic each)
+    (void)n_prim;
+    const unsigned b = wave_count(n_refl), c = wave_count(n_shadow);
     if (lane == 0) {
         const unsigned slot = ((blockIdx.y * gridDim.x + blockIdx.x) * (unsigned)WG_WAVES + (unsigned)wave) % COUNTER_SLOTS;
         unsigned long long* q = &p.counters[slot * 4];
-        if (a) atomicAdd(q + 0, (unsigned long long)a);
         if (b) atomicAdd(q + 1, (unsigned long long)b);
         if (c) atomicAdd(q + 2, (unsigned long long)c);
     }
