@@ -19,9 +19,12 @@ def main():
     ap.add_argument("--strip", default="", help="comma list of spheres,planes,lights to remove")
     ap.add_argument("--size", default="", help="WxH override")
     ap.add_argument("--inflight", type=int, default=1, help="frames in flight (streams/buffers)")
+    ap.add_argument("--lib", default="", help="library build to load instead of the in-tree one")
     a = ap.parse_args()
     import torch
-    from raytracer_hip import Context, scenes
+    from raytracer_hip import Context, abi, scenes
+    if a.lib:
+        abi.LIB_PATH = os.path.abspath(a.lib)
     sc = scenes.config(a.config)
     for what in filter(None, a.strip.split(",")):
         setattr(sc, what, [])
@@ -36,17 +39,18 @@ def main():
     for k in range(20):
         ctx.render_device(W, H, outs[k % a.inflight].data_ptr(), sp[k % a.inflight])
     torch.cuda.synchronize()
-    res = []
+    res, enq = [], []
     for _ in range(a.reps):
         t0 = time.perf_counter()
         for k in range(a.frames):
             ctx.render_device(W, H, outs[k % a.inflight].data_ptr(), sp[k % a.inflight])
+        enq.append((time.perf_counter() - t0) / a.frames * 1e6)
         torch.cuda.synchronize()
         res.append((time.perf_counter() - t0) / a.frames * 1e6)
     st = ctx.stats()
     kern = st["kernel_ms"] / st["launches"] * 1e3 if st["kernel_ms"] else float("nan")
-    print(f"{a.config} {W}x{H} strip={a.strip or '-'} inflight={a.inflight}: "
-          f"wall/frame min {min(res):.2f} us median {sorted(res)[len(res)//2]:.2f} us; event kernel avg {kern:.2f} us")
+    print(f"{os.path.basename(a.lib) or 'in-tree'} {a.config} {W}x{H} strip={a.strip or '-'} inflight={a.inflight}: "
+          f"wall/frame min {min(res):.2f} us median {sorted(res)[len(res)//2]:.2f} us; host enqueue/frame {min(enq):.2f} us")
 
 
 if __name__ == "__main__":
