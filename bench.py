@@ -257,16 +257,19 @@ def main():
             },
             "roofline_valu": {
                 "bound": "valu",
-                # issued VALU lane-slots: SQ_INSTS_VALU (wave instructions per launch, PMC) x 64
-                "achieved": valu_insts * 64 / kernel_s / 1e12 if valu_insts else None,
+                # chip-level issue rate: SQ_INSTS_VALU (wave instructions per launch, PMC) x 64
+                # lanes per frame, over the frame period (frames overlap when several are in flight)
+                "achieved": valu_insts * 64 / period_s / 1e12 if valu_insts else None,
                 "peak": VALU_PEAK_TOPS,
                 "unit": "TOP/s",
-                "frac": valu_insts * 64 / kernel_s / 1e12 / VALU_PEAK_TOPS if valu_insts else None,
+                "frac": valu_insts * 64 / period_s / 1e12 / VALU_PEAK_TOPS if valu_insts else None,
+                "achieved_per_launch": valu_insts * 64 / kernel_s / 1e12 if valu_insts else None,
                 "brute_force_equiv": brute_tops,
                 "brute_force_ops_per_launch": f_alg / steps / max(1, world),
-                "note": "achieved = issued VALU lane-ops (profiles/pmc_traffic.json SQ_INSTS_VALU x 64) / "
-                        "kernel time; brute_force_equiv = 24 ops per sphere test + 17 per plane test over "
-                        "every primitive (SURVEY.md 8d) / kernel time -- above peak where culling skips tests",
+                "note": "achieved = issued VALU lane-ops per frame (profiles/pmc_traffic.json SQ_INSTS_VALU x 64) / "
+                        "frame period; achieved_per_launch uses the launch duration instead; brute_force_equiv = "
+                        "24 ops per sphere test + 17 per plane test over every primitive (SURVEY.md 8d) / kernel "
+                        "time -- above peak where culling skips tests",
             },
             "cpu_baseline": None,
         }
