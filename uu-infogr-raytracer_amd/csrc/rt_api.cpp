@@ -85,6 +85,10 @@ struct Device {
     int32_t* d_frames2[2] = {nullptr, nullptr};  // rt_render_async double buffer
     size_t frames2_cap[2] = {0, 0};
     hipStream_t slot_stream[2] = {nullptr, nullptr};  // one per buffer: two frames in flight
+    float* d_view_tab = nullptr;  // lx[W] then ly[H] (view_tables)
+    size_t view_tab_cap = 0;
+    int tab_w = -1, tab_h = -1;
+    float tab_pw = 0, tab_ph = 0;
     int async_next = 0;
     unsigned long long* d_counters = nullptr;
     std::vector<EventPair> pending, pool;
@@ -325,6 +329,33 @@ void scene_params(const rt_ctx* ctx, const Device& d, LaunchParams& lp) {
     lp.counters = d.d_counters;
 }
 
+// Per-column / per-row view-plane coordinates of TracePixel (:963-965), computed with the
+// same binary32 operations as the kernel would (-ffp-contract=off, correctly rounded
+// division): lx[x] = ((float)x / W - 0.5f) * pw, ly[y] = ((float)y / H - 0.5f) * ph.
+// Rebuilt only when the frame size or view-plane size changes; frames in flight may read
+// the old table, so the device is synchronised first.
+int view_tables(rt_ctx* ctx, Device& d, LaunchParams& lp) {
+    if (d.tab_w != lp.W || d.tab_h != lp.H || d.tab_pw != lp.pw || d.tab_ph != lp.ph || !d.d_view_tab) {
+        std::vector<float> t((size_t)lp.W + (size_t)lp.H);
+        for (int x = 0; x < lp.W; ++x) {
+            const float px = (float)x / (float)lp.W - 0.5f;
+            t[(size_t)x] = px * lp.pw;
+        }
+        for (int y = 0; y < lp.H; ++y) {
+            const float py = (float)y / (float)lp.H - 0.5f;
+            t[(size_t)lp.W + (size_t)y] = py * lp.ph;
+        }
+        HIP_TRY(ctx, hipDeviceSynchronize());
+        int rc = grow(ctx, (void**)&d.d_view_tab, &d.view_tab_cap, t.size() * sizeof(float));
+        if (rc != RT_OK) return rc;
+        HIP_TRY(ctx, hipMemcpy(d.d_view_tab, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice));
+        d.tab_w = lp.W, d.tab_h = lp.H, d.tab_pw = lp.pw, d.tab_ph = lp.ph;
+    }
+    lp.lxt = d.d_view_tab;
+    lp.lyt = d.d_view_tab + lp.W;
+    return RT_OK;
+}
+
 // Launch the trace of bands (first, step) of `band_rows` rows into `out` on device d.
 int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int band_rows, int first, int step,
                 int32_t* out, int* n_bands) {
@@ -333,6 +364,8 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
     int rc = view_params(ctx, W, H, lp);
     if (rc != RT_OK) return rc;
     scene_params(ctx, d, lp);
+    rc = view_tables(ctx, d, lp);
+    if (rc != RT_OK) return rc;
     const int nb = bands_of(H, band_rows, first, step);
     if (n_bands) *n_bands = nb;
     lp.band_rows = band_rows, lp.band_first = first, lp.band_step = step;
@@ -457,6 +490,7 @@ void rt_destroy(rt_ctx* ctx) {
         for (int i = 0; i < 2; ++i)
             if (d.d_frames2[i]) (void)hipFree(d.d_frames2[i]);
         if (d.d_counters) (void)hipFree(d.d_counters);
+        if (d.d_view_tab) (void)hipFree(d.d_view_tab);
         for (hipStream_t s : d.slot_stream)
             if (s) (void)hipStreamDestroy(s);
         if (d.stream) (void)hipStreamDestroy(d.stream);

@@ -94,6 +94,8 @@ struct LaunchParams {
     const DevPlane* pl;
     const DevLight* li;
     const DevSphereCull* scull;  // [S]
+    const float* lxt;  // [W]: ((float)x / W - 0.5f) * pw, TracePixel :963-965
+    const float* lyt;  // [H]: ((float)y / H - 0.5f) * ph
     int S, P, L, limit;
     // view, RayTracer.cs:511-523 and :892-896 (computed on the host)
     float cam[3], right[3], up[3], fwd[3];

@@ -176,10 +176,12 @@ __device__ __forceinline__ float plane_t(f3 o, f3 d, const DevPlane& p) {
 }
 
 // ShiftColor, :1046-1052: Math.Clamp (NaN passes), * 255f, Math.Floor, (int), (byte).
+// Branch-free: IEEE maxNum/minNum return the non-NaN operand, so NaN -> 0 -> byte 0, the
+// byte .NET gives ((int)NaN = int.MinValue, (byte) of it = 0); +-inf clamp to 1 / 0 and -0
+// gives 0 as in the reference.
 __device__ __forceinline__ uint32_t shift_channel(float c) {
-    if (!(c == c)) return 0u;  // NaN -> (int) int.MinValue -> (byte) 0
-    const float cl = c < 0.0f ? 0.0f : (c > 1.0f ? 1.0f : c);
-    return (uint32_t)(int32_t)__builtin_floorf(cl * 255.0f) & 255u;
+    const float cl = __builtin_fminf(__builtin_fmaxf(c, 0.0f), 1.0f);
+    return (uint32_t)(int32_t)__builtin_floorf(cl * 255.0f);
 }
 
 // Per-lane level stack.  Records: a = {hit point, t}, b = {incoming direction, primitive code}.
@@ -720,9 +722,9 @@ __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p
     if (valid) {
         const f3 cam = mk(p.cam[0], p.cam[1], p.cam[2]);
         // TracePixel primary ray, :963-971 (no half-pixel offset)
-        const float px = (float)x / (float)p.W - 0.5f;
-        const float py = (float)y / (float)p.H - 0.5f;
-        const float lx = px * p.pw, ly = py * p.ph, lz = 1.0f * p.nearc;
+        // lx = ((float)x / W - 0.5f) * pw, ly likewise: per-column / per-row tables built on
+        // the host with the same binary32 operations (view_tables in rt_api.cpp)
+        const float lx = p.lxt[x], ly = p.lyt[y], lz = 1.0f * p.nearc;
         const f3 vp = add(add(add(cam, scale(mk(p.right[0], p.right[1], p.right[2]), lx)),
                               scale(mk(p.up[0], p.up[1], p.up[2]), ly)),
                           scale(mk(p.fwd[0], p.fwd[1], p.fwd[2]), lz));
@@ -1173,9 +1175,8 @@ __global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel(LaunchParams p
     unsigned cnt = 0;  // packed: reflected segments (bits 0-7) | shadow rays << CNT_SHADOW_SHIFT
     const f3 cam = mk(p.cam[0], p.cam[1], p.cam[2]);
     // TracePixel primary ray, :963-971 (no half-pixel offset)
-    const float px = (float)x / (float)p.W - 0.5f;
-    const float py = (float)y / (float)p.H - 0.5f;
-    const float lx = px * p.pw, ly = py * p.ph, lz = 1.0f * p.nearc;
+    // per-column / per-row tables (see the direct kernel); lanes outside the frame read 0
+    const float lx = valid ? p.lxt[x] : 0.0f, ly = valid ? p.lyt[y] : 0.0f, lz = 1.0f * p.nearc;
     const f3 vp = add(add(add(cam, scale(mk(p.right[0], p.right[1], p.right[2]), lx)),
                           scale(mk(p.up[0], p.up[1], p.up[2]), ly)),
                       scale(mk(p.fwd[0], p.fwd[1], p.fwd[2]), lz));
