@@ -509,6 +509,83 @@ static int32_t trace_pixel_nearest(const Scene* s, int x, int y, oracle_stats* s
 }
 
 /* ------------------------------------------------------------------------- */
+/* Float hit records of the visible path: every ray of every       */
+/* stride-th pixel as (origin, end, kind), in the order the pixel's walk       */
+/* produces them -- primary / reflected segment to its selected hit (origin +  */
+/* 100 * dir when nothing is selected), then at a shaded diffuse hit one       */
+/* shadow ray per light ending at the first sphere (scene order) that blocks   */
+/* it, at hit + t * light.position, else at t = 1.  The checker for            */
+/* rt_debug_segments.                                                         */
+/* ------------------------------------------------------------------------- */
+
+static void seg_put(rt_segment* out, int cap, int* n, v3 o, v3 e, int kind, int pixel) {
+    if (*n < cap) {
+        out[*n].origin = o;
+        out[*n].end = e;
+        out[*n].kind = kind;
+        out[*n].pixel = pixel;
+    }
+    ++*n;
+}
+
+static void segments_pixel(const Scene* s, int x, int y, rt_segment* out, int cap, int* n) {
+    const int pixel = y * s->width + x;
+    v3 o = s->cam_pos, d = primary_dir(s, x, y);
+    for (int level = 0;; ++level) {
+        const int primary = level == 0;
+        float best_s = INFINITY, best_p = INFINITY;
+        int win_s = -1, win_p = -1;
+        for (int i = 0; i < s->ns; ++i) {
+            float t = intersect_sphere(o, d, &s->sph[i], 0.0f).distance;
+            if (primary ? (t > 0 && best_s > t) : (t - 0.01f > 0 && t - 0.01f < best_s)) {
+                best_s = t;
+                win_s = i;
+            }
+        }
+        for (int i = 0; i < s->np; ++i) {
+            float t = intersect_plane(o, d, &s->pl[i]).distance;
+            if (t > 0 && t < best_p) {
+                best_p = t;
+                win_p = i;
+            }
+        }
+        int is_sphere, none = 0;
+        float t = 0;
+        if (best_s < best_p) {
+            is_sphere = 1;
+            t = best_s;
+        } else if (win_p >= 0) {
+            is_sphere = 0;
+            t = best_p;
+        } else {
+            is_sphere = 0;
+            none = 1;
+        }
+        seg_put(out, cap, n, o, vadd(o, vscale(d, none ? 100.0f : t)), primary ? 0 : 1, pixel);
+        if (none || t - 0.01f <= 0 || level > s->limit) return;
+        const v3 hp = vadd(o, vscale(d, t));
+        const rt_material* m = is_sphere ? &s->sph[win_s].m : &s->pl[win_p].m;
+        if (m_is_diffuse(m))
+            for (int li = 0; li < s->nl; ++li) {
+                const rt_light* l = &s->li[li];
+                float tb = 1.0f;
+                for (int i = 0; i < s->ns; ++i) {
+                    Isect r = intersect_sphere(hp, l->position, &s->sph[i], 0.001f);
+                    if (r.collision) {
+                        tb = r.distance;
+                        break;
+                    }
+                }
+                seg_put(out, cap, n, hp, vadd(hp, vscale(l->position, tb)), 2, pixel);
+            }
+        if (!m_is_mirror(m)) return;
+        const v3 normal = is_sphere ? vnormalize(vsub(hp, s->sph[win_s].center)) : s->pl[win_p].normal;
+        d = reflect(d, normal);
+        o = hp;
+    }
+}
+
+/* ------------------------------------------------------------------------- */
 /* Frame drivers                                                              */
 /* ------------------------------------------------------------------------- */
 
@@ -616,6 +693,42 @@ int oracle_render(const rt_sphere* spheres, int n_spheres, const rt_plane* plane
     }
     free(ws);
     free(th);
+    free(sph);
+    free(pl);
+    return RT_OK;
+}
+
+int oracle_segments(const rt_sphere* spheres, int n_spheres, const rt_plane* planes, int n_planes,
+                    const rt_light* lights, int n_lights, rt_vec3 ambient, int recursion_limit,
+                    const rt_camera* camera, int width, int height, int stride, rt_segment* out, int capacity,
+                    int* out_count) {
+    if (n_spheres < 0 || n_planes < 0 || n_lights < 0 || width <= 0 || height <= 0 || !camera || stride <= 0 ||
+        capacity < 0 || (capacity && !out) || !out_count || recursion_limit < 0 || (n_spheres && !spheres) ||
+        (n_planes && !planes) || (n_lights && !lights))
+        return RT_ERR_INVALID_ARG;
+    Sphere* sph = (Sphere*)calloc((size_t)(n_spheres ? n_spheres : 1), sizeof(Sphere));
+    Plane* pl = (Plane*)calloc((size_t)(n_planes ? n_planes : 1), sizeof(Plane));
+    for (int i = 0; i < n_spheres; ++i) {
+        sph[i].center = spheres[i].center;
+        sph[i].radius = spheres[i].radius;
+        sph[i].radius_sq = spheres[i].radius * spheres[i].radius;
+        sph[i].m = spheres[i].material;
+    }
+    for (int i = 0; i < n_planes; ++i) {
+        pl[i].center = planes[i].center;
+        pl[i].normal = planes[i].normal;
+        pl[i].m = planes[i].material;
+    }
+    Scene s;
+    memset(&s, 0, sizeof s);
+    s.sph = sph, s.ns = n_spheres, s.pl = pl, s.np = n_planes, s.li = lights, s.nl = n_lights;
+    s.ambient = ambient, s.limit = recursion_limit;
+    s.cam_pos = camera->position, s.yaw = camera->yaw, s.pitch = camera->pitch;
+    s.width = width, s.height = height, s.view_params = view_params(width, height);
+    int n = 0;
+    for (long long idx = 0; idx < (long long)width * height; idx += stride)
+        segments_pixel(&s, (int)(idx % width), (int)(idx / width), out, capacity, &n);
+    *out_count = n;
     free(sph);
     free(pl);
     return RT_OK;

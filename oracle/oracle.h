@@ -44,6 +44,15 @@ int oracle_render(const rt_sphere* spheres, int n_spheres,
                   int row_begin, int row_end,
                   int32_t* pixels, int mode, int nthreads, oracle_stats* stats);
 
+/* Visible-path segments (float hit records) of every stride-th pixel, in each pixel's walk
+ * order -- the checker for rt_debug_segments.  *out_count receives the total. */
+int oracle_segments(const rt_sphere* spheres, int n_spheres,
+                    const rt_plane* planes, int n_planes,
+                    const rt_light* lights, int n_lights,
+                    rt_vec3 ambient, int recursion_limit,
+                    const rt_camera* camera, int width, int height, int stride,
+                    rt_segment* out, int capacity, int* out_count);
+
 /* Per-function known-answer entry points. */
 float oracle_intersect_sphere(rt_vec3 origin, rt_vec3 direction, rt_vec3 center,
                               float radius, float epsilon, int* collision);

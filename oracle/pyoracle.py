@@ -58,11 +58,34 @@ def lib():
         l.oracle_shift_color.argtypes = [abi.rt_vec3]
         l.oracle_camera_view.restype = C.c_int
         l.oracle_camera_view.argtypes = [C.POINTER(abi.rt_camera), C.c_int, C.c_int, C.POINTER(abi.rt_view)]
+        l.oracle_segments.restype = C.c_int
+        l.oracle_segments.argtypes = [C.POINTER(abi.rt_sphere), C.c_int, C.POINTER(abi.rt_plane), C.c_int,
+                                      C.POINTER(abi.rt_light), C.c_int, abi.rt_vec3, C.c_int,
+                                      C.POINTER(abi.rt_camera), C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                      C.POINTER(C.c_int)]
         l.oracle_net_float_to_int.restype = C.c_int32
         l.oracle_net_float_to_int.argtypes = [C.c_float]
         l.abi = abi
         _lib = l
     return _lib
+
+
+def segments(scene, stride=1):
+    """Visible-path segments (float hit records) of every stride-th pixel, in each pixel's walk
+    order, as a numpy array of raytracer_hip.SEGMENT_DTYPE (oracle_segments)."""
+    from raytracer_hip.debugview import SEGMENT_DTYPE
+    l = lib()
+    S, P, L = scene.c_arrays()
+    cam = scene.c_camera()
+    n = C.c_int(0)
+    args = (S, len(scene.spheres), P, len(scene.planes), L, len(scene.lights), l.abi.rt_vec3(*scene.ambient),
+            scene.recursion_limit, C.byref(cam), scene.width, scene.height, stride)
+    if l.oracle_segments(*args, None, 0, C.byref(n)) != 0:
+        raise RuntimeError("oracle_segments failed")
+    out = np.zeros(n.value, dtype=SEGMENT_DTYPE)
+    if l.oracle_segments(*args, out.ctypes.data, n.value, C.byref(n)) != 0:
+        raise RuntimeError("oracle_segments failed")
+    return out
 
 
 def render(scene, mode=MODE_NEAREST, nthreads=None, rows=None, width=None, height=None):

@@ -366,3 +366,27 @@ def test_two_frames_in_flight_on_two_streams(gpu_ctx, golden):
         gpu_ctx.render_device(sc.width, sc.height, outs[k % 2].data_ptr(), streams[k % 2].cuda_stream)
     torch.cuda.synchronize()
     assert all(crc(o.cpu().numpy()) == e["crc32"] for o in outs)
+
+
+def _segment_scenes():
+    from random_scenes import camera_sweep_scene, random_scene
+    out = [scenes.reference(96, 64), scenes.config("C3").resized(80, 45), scenes.config("C4").resized(64, 36)]
+    out += [random_scene(s) for s in range(8)] + [random_scene(s, dense=True) for s in range(100, 104)]
+    out += [camera_sweep_scene(s, 96, 64) for s in range(0, 12)]
+    return out
+
+
+@pytest.mark.parametrize("k", list(range(27)))
+def test_debug_segments_are_the_oracle_hit_records(gpu_ctx, oracle, k):
+    """Float hit records, 0 ulp: every visible-path segment of every pixel --
+    origin, hit point / shadow-blocker point, kind -- bit-identical to oracle_segments."""
+    sc = _segment_scenes()[k]
+    want = oracle.segments(sc)
+    gpu_ctx.set_scene(sc)
+    got, total = gpu_ctx.debug_segments(sc.width, sc.height, sample_stride=1, capacity=len(want) + 64)
+    assert total == len(want)
+    got = got[np.argsort(got["pixel"], kind="stable")]  # per-lane appends keep each pixel's order
+    if got.tobytes() != want.tobytes():
+        diff = np.nonzero([a.tobytes() != b.tobytes() for a, b in zip(got, want)])[0]
+        i = int(diff[0])
+        pytest.fail(f"{sc.name}: {len(diff)} of {len(want)} records differ; first #{i}: gpu {got[i]} oracle {want[i]}")

@@ -157,3 +157,17 @@ def test_dense_random_scenes_oracle_drivers(oracle, seed):
     ref, _ = oracle.render(sc, oracle.MODE_REFERENCE, 4)
     near, _ = oracle.render(sc, oracle.MODE_NEAREST, 4)
     assert np.array_equal(ref, near)
+
+
+@pytest.mark.parametrize("cid,w,h", [("REF", 96, 64), ("C3", 80, 45), ("C4", 48, 27)])
+def test_oracle_segments_count_every_visible_ray(oracle, cid, w, h):
+    """oracle_segments (float hit records): one record per visible-path ray."""
+    from raytracer_hip import scenes
+    sc = scenes.config(cid).resized(w, h)
+    seg = oracle.segments(sc)
+    _, st = oracle.render(sc, oracle.MODE_NEAREST, 2)
+    assert np.bincount(seg["kind"], minlength=3).tolist() == [st["primary_rays"], st["reflect_rays"],
+                                                                 st["shadow_rays"]]
+    prim = seg[seg["kind"] == 0]
+    assert np.array_equal(prim["pixel"], np.arange(w * h))
+    assert np.all(np.diff(seg["pixel"]) >= 0)  # walk order, pixel by pixel
