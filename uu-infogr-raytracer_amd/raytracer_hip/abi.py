@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
 LIB_PATH = os.path.join(PKG_ROOT, "lib", "libraytracer_hip.so")
 
+RT_ABI_VERSION = 2  # include/raytracer_hip.h
 RT_OK = 0
 RT_ERR_INVALID_ARG = -1
 RT_ERR_NO_DEVICE = -2
