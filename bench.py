@@ -44,6 +44,12 @@ def parse():
                          "slot; every frame is fully traced)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="N>1: gather each frame before tracing the next (no double buffering)")
+    ap.add_argument("--batch", type=int, default=8,
+                    help="N>1: frames per RCCL gather (double-buffered; 1 = one gather per frame)")
+    ap.add_argument("--band-format", choices=["rgb24", "int32"], default="rgb24",
+                    help="N>1: band sets shipped to rank 0 as packed 24-bit RGB or int32 pixels")
+    ap.add_argument("--dist-path", action="store_true",
+                    help="rehearsal: run the N>1 band/gather path even with one process (RCCL world of 1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
@@ -111,9 +117,12 @@ def main():
     if not os.path.exists(abi.LIB_PATH):
         subprocess.run(["make", "-s", "-C", os.path.join(PKG, "csrc")], check=True)
 
-    if world > 1:
+    distributed = world > 1 or args.dist_path
+    if distributed:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29531")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     sc = scenes.config(args.config)
@@ -127,7 +136,7 @@ def main():
         pass
 
     streams = [stream]
-    if world == 1:
+    if not distributed:
         nf = max(1, args.inflight)
         frames = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in range(nf)]
         streams += [torch.cuda.Stream() for _ in range(nf - 1)]
@@ -141,7 +150,7 @@ def main():
             k_step[0] = k + 1
             ctx.render_device(W, H, frames[k % nf].data_ptr(), streams[k % nf].cuda_stream)
     else:
-        from raytracer_hip.dist import BandGather, PipelinedBandGather, RowBands
+        from raytracer_hip.dist import BandGather, BatchedBandGather, RowBands
         rb = RowBands(W, H, args.band_rows, rank, world)
         px_per_launch = rb.pixels
         frame = torch.empty(W * H, dtype=torch.int32, device="cuda") if rank == 0 else None
@@ -159,15 +168,48 @@ def main():
                 ctx.render_bands(W, H, rb.band_rows, rank, world, bg.local.data_ptr(), s)
                 scatter(bg.gather())
         else:
-            pg = PipelinedBandGather(rb, torch.device("cuda", local))
+            fmt = abi.RT_BANDS_RGB24 if args.band_format == "rgb24" else abi.RT_BANDS_INT32
+            bgb = BatchedBandGather(rb, torch.device("cuda", local), frames_per_batch=args.batch,
+                                    bpp=3 if fmt == abi.RT_BANDS_RGB24 else 4)
+
+            def reassemble(done):
+                # rank 0: one launch per frame puts every rank's bands into the frame
+                if rank == 0:
+                    for buf, n in done:
+                        for f in range(n):
+                            ctx.scatter_gathered(W, H, rb.band_rows, world, buf.data_ptr() + f * bgb.slot_bytes,
+                                                 bgb.rank_stride, frame.data_ptr(), fmt, s)
+
+            # frames of a batch alternate between trace streams (two frames in flight per rank);
+            # the batch's gather is issued on `stream` after it has joined the others, and every
+            # trace stream waits for the previous gather (whose buffer the next batch reuses)
+            tstreams = [stream] + [torch.cuda.Stream() for _ in range(max(1, args.inflight) - 1)]
+
+            def join_traces():
+                for t in tstreams[1:]:
+                    stream.wait_stream(t)
+
+            def after_gather_wait():
+                for t in tstreams[1:]:
+                    t.wait_stream(stream)
 
             def step():
-                # trace frame k into one slot while frame k-1's RCCL gather is in flight
-                ctx.render_bands(W, H, rb.band_rows, rank, world, pg.buffer().data_ptr(), s)
-                scatter(pg.submit())
+                # trace frame k's bands into its slot of the current batch; every F frames one
+                # gather ships the batch to rank 0 while the next batch is traced
+                k = bgb.k
+                ctx.render_bands_ex(W, H, rb.band_rows, rank, world, bgb.frame_buffer(), fmt,
+                                    tstreams[k % len(tstreams)].cuda_stream)
+                if (k + 1) % bgb.F == 0:
+                    join_traces()
+                done = bgb.commit()
+                if (k + 1) % bgb.F == 0:
+                    after_gather_wait()
+                if done is not None:
+                    reassemble([done])
 
-            def finish():  # noqa: F811  -- the last frame's gather and reassembly
-                scatter(pg.drain())
+            def finish():  # noqa: F811  -- the last (possibly partial) batch
+                join_traces()
+                reassemble(bgb.drain())
 
     for _ in range(args.warmup):
         step()
@@ -175,7 +217,7 @@ def main():
     torch.cuda.synchronize()
     ctx.reset_stats()
 
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -190,7 +232,7 @@ def main():
         stream.wait_stream(st_)
     ev1.record(stream)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
 
@@ -203,7 +245,7 @@ def main():
     sampled_s = st["kernel_ms"] / 1e3 / max(1, st["timed_launches"])
     period_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
     kernel_s = sampled_s if st["timed_launches"] else period_s
-    if world > 1:
+    if distributed:
         t = torch.tensor([elapsed, float(rays), float(f_alg), kernel_s], dtype=torch.float64, device="cuda")
         tmax = t.clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
@@ -237,9 +279,11 @@ def main():
                 "workload": f"{sc.name}: {sc.note}",
                 "width": W, "height": H, "spheres": len(sc.spheres), "planes": len(sc.planes),
                 "lights": len(sc.lights), "depth": sc.recursion_limit + 1,
-                "parallelism": f"single GPU, {max(1, args.inflight)} frames in flight" if world == 1 else
+                "parallelism": f"single GPU, {max(1, args.inflight)} frames in flight" if not distributed else
                 f"interleaved {args.band_rows}-row bands x {world} ranks + RCCL gather to rank 0"
-                + ("" if args.no_pipeline else " (double-buffered: gather k overlaps trace k+1)"),
+                + (" (one gather per frame)" if args.no_pipeline else
+                   f" ({args.batch} frames per gather, {args.band_format} bands, double-buffered: the gather of "
+                   f"one batch overlaps the trace of the next)"),
                 "rays_per_frame": rays_per_frame,
             },
             "roofline": {
@@ -289,7 +333,7 @@ def main():
                 out["cpu_baseline"] = cpu_baseline(sc, rays_per_frame, args.cpu_seconds)
         print(json.dumps(out), flush=True)
     ctx.close()
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 2
+#define RT_ABI_VERSION 3
 
 /* ---- status codes ---------------------------------------------------------- */
 enum {
@@ -195,6 +195,20 @@ int rt_render_bands(rt_ctx* ctx, int width, int height, int band_rows, int band_
  * Asynchronous on hip_stream. */
 int rt_scatter_bands(rt_ctx* ctx, int width, int height, int band_rows, int band_first,
                      int band_step, const int32_t* d_bands, int32_t* d_frame, void* hip_stream);
+
+/* Band sets for shipping to rank 0.  Formats: RT_BANDS_INT32 (as
+ * rt_render_bands) or RT_BANDS_RGB24 (3 bytes B, G, R per pixel: the top byte of
+ * 0x00RRGGBB is always 0, so a quarter fewer bytes cross xGMI). */
+enum { RT_BANDS_INT32 = 0, RT_BANDS_RGB24 = 1 };
+int rt_render_bands_ex(rt_ctx* ctx, int width, int height, int band_rows, int band_first,
+                       int band_step, void* d_out, int format, void* hip_stream, int* out_n_bands);
+/* Reassemble the band sets of `world` ranks (band b rendered by rank b % world with
+ * band_first = rank, band_step = world), gathered rank after rank at slot_bytes intervals
+ * in d_gathered, into the row-major frame d_frame[height][width] -- one launch for all
+ * ranks (rank 0's side of the RCCL gather). */
+int rt_scatter_gathered(rt_ctx* ctx, int width, int height, int band_rows, int world,
+                        const void* d_gathered, size_t slot_bytes, int format, int32_t* d_frame,
+                        void* hip_stream);
 
 /* ---- double-buffered frames ------------------------------ */
 /* Asynchronous Tick(): captures the current camera, enqueues the trace and the D2H copy

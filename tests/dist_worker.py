@@ -95,3 +95,62 @@ def run_pipelined(rank, world, port, cfg, width, height, band_rows, frames, resu
         dist.barrier()
     finally:
         dist.destroy_process_group()
+
+
+def run_batched(rank, world, port, cfg, width, height, band_rows, frames, per_batch, result_path):
+    """bench.py's N>1 step: F frames per gather, RGB24 band sets, rank 0 reassembles every
+    frame with the host mirror of rt_scatter_gathered and checks it against the oracle."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path[:0] = [os.path.join(root, "uu-infogr-raytracer_amd"), os.path.join(root, "oracle"), here]
+    import ctypes
+    import numpy as np
+    import torch.distributed as dist
+
+    import pyoracle
+    from raytracer_hip import scenes
+    from raytracer_hip.dist import BatchedBandGather, RowBands, pack_rgb24, scatter_gathered_host
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        base = scenes.config(cfg).resized(width, height)
+
+        def scene_for(k):
+            sc = base.resized(width, height)
+            sc.camera = ((0.0, 0.0, 0.0), 0.04 * k - 0.1, -0.02 * k)
+            return sc
+
+        rb = RowBands(width, height, band_rows, rank, world)
+        g = BatchedBandGather(rb, "cpu", frames_per_batch=per_batch)
+        got = []
+
+        def consume(done):
+            for buf, n in done:
+                host = buf.numpy()
+                for f in range(n):
+                    got.append(scatter_gathered_host(host[f * g.slot_bytes:], g.rank_stride, width, height,
+                                                     band_rows, world))
+
+        for k in range(frames):
+            ptr = g.frame_buffer()
+            dst = (ctypes.c_uint8 * g.slot_bytes).from_address(ptr)
+            slot = np.frombuffer(dst, dtype=np.uint8)
+            slot[:] = 0xEE
+            for l0, y0, n in rb.row_spans():
+                rows, _ = pyoracle.render(scene_for(k), pyoracle.MODE_NEAREST, 2, rows=(y0, y0 + n))
+                b = pack_rgb24(rows)
+                slot[l0 * width * 3:l0 * width * 3 + b.size] = b
+            done = g.commit()
+            if done is not None and rank == 0:
+                consume([done])
+        rest = g.drain()
+        if rank == 0:
+            consume(rest)
+            bad = [k for k, fr in enumerate(got)
+                   if not np.array_equal(fr, pyoracle.render(scene_for(k), pyoracle.MODE_NEAREST, 2)[0])]
+            with open(result_path, "w") as f:
+                f.write("ok" if len(got) == frames and not bad else f"bad frames {bad} of {len(got)}")
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()

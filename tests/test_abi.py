@@ -56,7 +56,7 @@ def test_struct_layouts_match_header():
 
 
 def test_abi_version(rtlib):
-    assert rtlib.rt_abi_version() == 2 == abi.RT_ABI_VERSION
+    assert rtlib.rt_abi_version() == 3 == abi.RT_ABI_VERSION
     hdr = open(HEADER).read()
     assert re.search(r"#define RT_ABI_VERSION (\d+)", hdr).group(1) == str(abi.RT_ABI_VERSION)
 

@@ -85,3 +85,42 @@ def test_gloo_pipelined_gather_keeps_frames_apart(tmp_path, world, frames):
             p.kill()
     assert codes == [0] * world, codes
     assert result.read_text() == "ok"
+
+
+@pytest.mark.parametrize("world,frames,per_batch", [(2, 7, 3), (3, 5, 2), (2, 4, 4)])
+def test_gloo_batched_rgb24_gather(tmp_path, world, frames, per_batch):
+    """F frames per gather, RGB24 bands, one reassembly per frame (bench.py's N>1 step);
+    the last batch may be partial."""
+    import dist_worker
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    result = tmp_path / "result.txt"
+    procs = [ctx.Process(target=dist_worker.run_batched,
+                         args=(r, world, port, "C3", 40, 29, 4, frames, per_batch, str(result))) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0] * world, codes
+    assert result.read_text() == "ok"
+
+
+def test_scatter_gathered_host_matches_scatter_host():
+    from raytracer_hip.dist import pack_rgb24, scatter_gathered_host
+    W, H, br, world = 11, 23, 3, 4
+    frame = (np.arange(W * H, dtype=np.int32) * 0x01F3A7) & 0xFFFFFF
+    frame = frame.reshape(H, W)
+    for bpp in (3, 4):
+        stride = 1000
+        buf = np.zeros(world * stride, dtype=np.uint8)
+        for r in range(world):
+            rb = RowBands(W, H, br, r, world)
+            for l0, y0, n in rb.row_spans():
+                rows = frame[y0:y0 + n]
+                b = pack_rgb24(rows) if bpp == 3 else rows.astype(np.int32).view(np.uint8).reshape(-1)
+                buf[r * stride + l0 * W * bpp:r * stride + l0 * W * bpp + b.size] = b
+        assert np.array_equal(scatter_gathered_host(buf, stride, W, H, br, world, bpp), frame)

@@ -390,3 +390,25 @@ def test_debug_segments_are_the_oracle_hit_records(gpu_ctx, oracle, k):
         diff = np.nonzero([a.tobytes() != b.tobytes() for a, b in zip(got, want)])[0]
         i = int(diff[0])
         pytest.fail(f"{sc.name}: {len(diff)} of {len(want)} records differ; first #{i}: gpu {got[i]} oracle {want[i]}")
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 5, 8])
+@pytest.mark.parametrize("fmt", [0, 1])
+def test_band_sets_and_one_launch_reassembly(gpu_ctx, golden, world, fmt):
+    """rt_render_bands_ex (int32 / RGB24) per simulated rank into one gathered buffer, then
+    rt_scatter_gathered: the full frame, bit-exact."""
+    import torch
+    e = golden["cases"]["C3_96x54"]
+    sc = scenes.config(e["config"]).resized(e["width"], e["height"])
+    W, H, br = sc.width, sc.height, 8
+    gpu_ctx.set_scene(sc)
+    bpp = 4 if fmt == 0 else 3
+    stride = (bands_of(H, br, 0, world) * br * W * bpp + 255) // 256 * 256 + 512  # padded like dist.py
+    g = torch.full((world * stride,), 0xEE, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    for r in range(world):
+        gpu_ctx.render_bands_ex(W, H, br, r, world, g.data_ptr() + r * stride, fmt, s)
+    frame = torch.full((W * H,), -1, dtype=torch.int32, device="cuda")
+    gpu_ctx.scatter_gathered(W, H, br, world, g.data_ptr(), stride, frame.data_ptr(), fmt, s)
+    torch.cuda.synchronize()
+    assert crc(frame.cpu().numpy()) == e["crc32"]

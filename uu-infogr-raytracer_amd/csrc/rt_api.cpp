@@ -358,7 +358,7 @@ int view_tables(rt_ctx* ctx, Device& d, LaunchParams& lp) {
 
 // Launch the trace of bands (first, step) of `band_rows` rows into `out` on device d.
 int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int band_rows, int first, int step,
-                int32_t* out, int* n_bands) {
+                int32_t* out, int* n_bands, int fmt = RT_BANDS_INT32) {
     LaunchParams lp;
     std::memset(&lp, 0, sizeof lp);
     int rc = view_params(ctx, W, H, lp);
@@ -371,6 +371,7 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
     lp.band_rows = band_rows, lp.band_first = first, lp.band_step = step;
     lp.local_rows = nb * band_rows;
     lp.out = out;
+    lp.out_fmt = fmt;
     hipStream_t saved = d.stream;
     d.stream = stream;
     const bool timed = begin_timed(ctx, d, 0);
@@ -677,16 +678,23 @@ int rt_render_device(rt_ctx* ctx, int width, int height, int32_t* d_pixels, void
 
 int rt_render_bands(rt_ctx* ctx, int width, int height, int band_rows, int band_first, int band_step,
                     int32_t* d_out, void* hip_stream, int* out_n_bands) {
+    return rt_render_bands_ex(ctx, width, height, band_rows, band_first, band_step, d_out, RT_BANDS_INT32, hip_stream,
+                              out_n_bands);
+}
+
+int rt_render_bands_ex(rt_ctx* ctx, int width, int height, int band_rows, int band_first, int band_step, void* d_out,
+                       int format, void* hip_stream, int* out_n_bands) {
     int rc = check_ctx(ctx, width, height);
     if (rc != RT_OK) return rc;
-    if (band_rows <= 0 || band_first < 0 || band_step <= 0 || !d_out)
+    if (band_rows <= 0 || band_first < 0 || band_step <= 0 || !d_out ||
+        (format != RT_BANDS_INT32 && format != RT_BANDS_RGB24))
         return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_bands: bad band arguments");
     if (ctx->n_gpus != 1) return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_bands needs a single-GPU context");
     Device& d = ctx->dev[0];
     DeviceGuard guard(d.id);
     hipStream_t s = (hipStream_t)hip_stream;  // NULL = the HIP null stream
     int nb = 0;
-    rc = trace_bands(ctx, d, s, width, height, band_rows, band_first, band_step, d_out, &nb);
+    rc = trace_bands(ctx, d, s, width, height, band_rows, band_first, band_step, (int32_t*)d_out, &nb, format);
     if (out_n_bands) *out_n_bands = nb;
     if (rc == RT_OK) ctx->pixels += (uint64_t)nb * band_rows * width;
     return rc;
@@ -702,6 +710,22 @@ int rt_scatter_bands(rt_ctx* ctx, int width, int height, int band_rows, int band
     hipStream_t s = (hipStream_t)hip_stream;  // NULL = the HIP null stream
     const int nb = bands_of(height, band_rows, band_first, band_step);
     int e = launch_scatter_bands(d_bands, d_frame, width, height, band_rows, band_first, band_step, nb, s);
+    if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "scatter launch: %s", hipGetErrorString((hipError_t)e));
+    return RT_OK;
+}
+
+int rt_scatter_gathered(rt_ctx* ctx, int width, int height, int band_rows, int world, const void* d_gathered,
+                        size_t slot_bytes, int format, int32_t* d_frame, void* hip_stream) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "NULL context");
+    const size_t bpp = format == RT_BANDS_INT32 ? 4 : 3;
+    if (width <= 0 || height <= 0 || band_rows <= 0 || world <= 0 || !d_gathered || !d_frame ||
+        (format != RT_BANDS_INT32 && format != RT_BANDS_RGB24) ||
+        slot_bytes < (size_t)bands_of(height, band_rows, 0, world) * band_rows * width * bpp)
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_scatter_gathered: bad arguments");
+    Device& d = ctx->dev[0];
+    DeviceGuard guard(d.id);
+    int e = launch_scatter_gathered((const unsigned char*)d_gathered, slot_bytes, format, d_frame, width, height,
+                                    band_rows, world, hip_stream);
     if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "scatter launch: %s", hipGetErrorString((hipError_t)e));
     return RT_OK;
 }

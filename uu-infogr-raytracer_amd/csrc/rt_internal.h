@@ -105,6 +105,7 @@ struct LaunchParams {
     // global row = band * band_rows + r % band_rows; pixel written at out[r * W + x].
     int band_rows, band_first, band_step, local_rows;
     int32_t* out;
+    int out_fmt;  // 0: int32 0x00RRGGBB per pixel; 1: packed 24-bit (bytes B, G, R) per pixel
     unsigned long long* counters;  // COUNTER_SLOTS x {primary, reflect, shadow, pad}
     int prim_const;                // 1: pc[0..S) and pbox[0..S) valid (S <= MAX_PRIM_CONST)
     PrimConst pc[MAX_PRIM_CONST];
@@ -122,6 +123,9 @@ int launch_debug_segments(const LaunchParams& p, int stride, DevSegment* out, in
                           void* stream);
 // generic_pow: some material needs the f64 Math.Pow path (exponent not 0.5, 1 or 2).
 int launch_trace(const LaunchParams& p, bool generic_pow, void* stream);
+// All ranks' gathered band sets (rank r's at g + r * slot_bytes, format fmt) -> frame.
+int launch_scatter_gathered(const unsigned char* g, size_t slot_bytes, int fmt, int32_t* frame, int W, int H,
+                            int band_rows, int world, void* stream);
 int launch_scatter_bands(const int32_t* bands, int32_t* frame, int W, int H, int band_rows, int band_first,
                          int band_step, int n_bands, void* stream);
 

@@ -184,6 +184,19 @@ __device__ __forceinline__ uint32_t shift_channel(float c) {
     return (uint32_t)(int32_t)__builtin_floorf(cl * 255.0f);
 }
 
+// Frame / band output: int32 0x00RRGGBB, or packed 24-bit (B, G, R bytes; the top byte of
+// the int32 is always 0) for band sets shipped to rank 0 -- a quarter fewer bytes over xGMI.
+__device__ __forceinline__ void store_pixel(const LaunchParams& p, size_t i, uint32_t px32) {
+    if (p.out_fmt == 0) {
+        p.out[i] = (int32_t)px32;
+    } else {
+        unsigned char* o = (unsigned char*)p.out + i * 3;
+        o[0] = (unsigned char)px32;
+        o[1] = (unsigned char)(px32 >> 8);
+        o[2] = (unsigned char)(px32 >> 16);
+    }
+}
+
 // Per-lane level stack.  Records: a = {hit point, t}, b = {incoming direction, primitive code}.
 template <int K, bool SCRATCH>
 struct LevelStack;
@@ -776,7 +789,7 @@ __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p
                               &cnt);
         }
         const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
-        p.out[(size_t)r * (size_t)p.W + (size_t)x] = (int32_t)px32;
+        store_pixel(p, (size_t)r * (size_t)p.W + (size_t)x, px32);
     }
 
     add_counters(p, lane, wave, valid ? 1u : 0u, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT);
@@ -1254,7 +1267,7 @@ __global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel(LaunchParams p
     }
     if (valid) {
         const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
-        p.out[(size_t)r * (size_t)p.W + (size_t)x] = (int32_t)px32;
+        store_pixel(p, (size_t)r * (size_t)p.W + (size_t)x, px32);
     }
 
     add_counters(p, lane, wave, valid ? 1u : 0u, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT);
@@ -1334,6 +1347,30 @@ __global__ __launch_bounds__(256) void scatter_bands_kernel(const int32_t* __res
     }
 }
 
+// Reassemble every rank's gathered band set into the row-major frame in one launch:
+// frame row y is band b = y / band_rows, owned by rank b % world as its (b / world)-th band.
+__global__ __launch_bounds__(256) void scatter_gathered_kernel(const unsigned char* __restrict__ g, size_t slot_bytes,
+                                                               int fmt, int32_t* __restrict__ frame, int W, int H,
+                                                               int band_rows, int world) {
+    const size_t total = (size_t)W * (size_t)H;
+    for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < total; i += (size_t)gridDim.x * blockDim.x) {
+        const int y = (int)(i / (size_t)W);
+        const int x = (int)(i - (size_t)y * W);
+        const int b = y / band_rows;
+        const int rank = b % world;
+        const size_t local = ((size_t)(b / world) * band_rows + (size_t)(y % band_rows)) * (size_t)W + (size_t)x;
+        const unsigned char* src = g + (size_t)rank * slot_bytes;
+        int32_t v;
+        if (fmt == 0) {
+            v = ((const int32_t*)src)[local];
+        } else {
+            const unsigned char* q = src + local * 3;
+            v = (int32_t)((uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16));
+        }
+        frame[i] = v;
+    }
+}
+
 #define RT_DEFINE_DISPATCH(FN, NAME, ...)                                                        \
     template <bool GPOW>                                                                         \
     static void FN(const LaunchParams& p, dim3 grid, dim3 block, hipStream_t s) {                \
@@ -1379,6 +1416,17 @@ int launch_debug_segments(const LaunchParams& p, int stride, DevSegment* out, in
     if (n <= 0) return (int)hipSuccess;
     hipLaunchKernelGGL(debug_segments_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream, p,
                        stride, out, capacity, count);
+    return (int)hipGetLastError();
+}
+
+int launch_scatter_gathered(const unsigned char* g, size_t slot_bytes, int fmt, int32_t* frame, int W, int H,
+                            int band_rows, int world, void* stream) {
+    const size_t total = (size_t)W * (size_t)H;
+    if (total == 0) return (int)hipSuccess;
+    size_t blocks = (total + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    hipLaunchKernelGGL(scatter_gathered_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, g,
+                       slot_bytes, fmt, frame, W, H, band_rows, world);
     return (int)hipGetLastError();
 }
 

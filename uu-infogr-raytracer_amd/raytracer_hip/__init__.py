@@ -133,6 +133,19 @@ class Context:
         self._check(self.lib.rt_scatter_bands(self.ptr, width, height, band_rows, band_first, band_step,
                                               C.c_void_p(d_bands), C.c_void_p(d_frame), C.c_void_p(stream)))
 
+    def render_bands_ex(self, width: int, height: int, band_rows: int, band_first: int, band_step: int, d_ptr: int,
+                        fmt: int = abi.RT_BANDS_RGB24, stream: int = 0) -> int:
+        nb = C.c_int(0)
+        self._check(self.lib.rt_render_bands_ex(self.ptr, width, height, band_rows, band_first, band_step,
+                                                C.c_void_p(d_ptr), fmt, C.c_void_p(stream), C.byref(nb)))
+        return nb.value
+
+    def scatter_gathered(self, width: int, height: int, band_rows: int, world: int, d_gathered: int,
+                         rank_stride: int, d_frame: int, fmt: int = abi.RT_BANDS_RGB24, stream: int = 0):
+        """Reassemble all ranks' band sets (rank r's at d_gathered + r * rank_stride) into d_frame."""
+        self._check(self.lib.rt_scatter_gathered(self.ptr, width, height, band_rows, world, C.c_void_p(d_gathered),
+                                                 rank_stride, fmt, C.c_void_p(d_frame), C.c_void_p(stream)))
+
     def render_async(self, width: int, height: int, out: np.ndarray):
         """Double-buffered Tick (rt_render_async): returns at once; `wait()` before reading `out`."""
         assert out.dtype == np.int32 and out.flags.c_contiguous and out.size == width * height

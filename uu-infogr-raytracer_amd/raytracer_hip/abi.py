@@ -13,7 +13,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
 LIB_PATH = os.path.join(PKG_ROOT, "lib", "libraytracer_hip.so")
 
-RT_ABI_VERSION = 2  # include/raytracer_hip.h
+RT_ABI_VERSION = 3  # include/raytracer_hip.h
+RT_BANDS_INT32, RT_BANDS_RGB24 = 0, 1
 RT_OK = 0
 RT_ERR_INVALID_ARG = -1
 RT_ERR_NO_DEVICE = -2
@@ -101,6 +102,10 @@ EXPORTS = [
                                   C.c_void_p, C.POINTER(C.c_int)]),
     ("rt_scatter_bands", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                    C.c_void_p, C.c_void_p]),
+    ("rt_render_bands_ex", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                     C.c_void_p, C.POINTER(C.c_int)]),
+    ("rt_scatter_gathered", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_size_t,
+                                      C.c_int, C.c_void_p, C.c_void_p]),
     ("rt_render_async", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     ("rt_wait", C.c_int, [C.c_void_p]),
     ("rt_write_ppm", C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),

@@ -49,6 +49,29 @@ class RowBands:
         return out
 
 
+def pack_rgb24(pixels) -> np.ndarray:
+    """Host mirror of RT_BANDS_RGB24: int32 0x00RRGGBB -> bytes B, G, R per pixel."""
+    v = np.ascontiguousarray(pixels, dtype=np.int32).reshape(-1).view(np.uint8).reshape(-1, 4)
+    return np.ascontiguousarray(v[:, :3]).reshape(-1)
+
+
+def scatter_gathered_host(buf, rank_stride: int, width: int, height: int, band_rows: int, world: int,
+                          bpp: int = 3) -> np.ndarray:
+    """Host mirror of rt_scatter_gathered: rank r's band set at byte r * rank_stride of buf."""
+    buf = np.asarray(buf, dtype=np.uint8).reshape(-1)
+    frame = np.full((height, width), -1, dtype=np.int32)
+    for y in range(height):
+        b = y // band_rows
+        r, k = b % world, b // world
+        o = r * rank_stride + ((k * band_rows + y % band_rows) * width) * bpp
+        row = buf[o:o + width * bpp].reshape(width, bpp)
+        if bpp == 4:
+            frame[y] = row.view(np.int32).reshape(-1)
+        else:
+            frame[y] = row[:, 0].astype(np.int32) | (row[:, 1].astype(np.int32) << 8) | (row[:, 2].astype(np.int32) << 16)
+    return frame
+
+
 def scatter_host(parts, width: int, height: int, band_rows: int) -> np.ndarray:
     """Host mirror of rt_scatter_bands for every rank's gathered slot (rank order)."""
     world = len(parts)
@@ -126,3 +149,80 @@ class PipelinedBandGather:
         pw.wait()
         self.pending = None
         return self.parts[pi]
+
+
+class BatchedBandGather:
+    """F frames per RCCL gather, double-buffered (bench.py's N > 1 step).
+
+    Each rank renders frame k's bands (RT_BANDS_RGB24 by default: 3 bytes per pixel) into
+    slot k % F of the current batch buffer; after F frames one gather moves the whole batch to
+    rank 0 -- one collective's latency per F frames -- while the next batch is traced.  On
+    rank 0 the gathered buffer holds rank r's batch at r * rank_stride (rank_stride =
+    F * slot_bytes), so frame f of the batch is reassembled by ONE rt_scatter_gathered
+    launch from offset f * slot_bytes with rank stride rank_stride.
+
+        buf = g.frame_buffer()   -> device pointer for this rank's frame k
+        done = g.commit()        -> after frame k; (gathered tensor, n_frames) of the batch
+                                    completed earlier (rank 0) or None
+        done = g.drain()         -> at the end: submits a partial batch, returns what is left
+    Ordering on GPUs (ProcessGroupNCCL): a gather waits for the current stream's earlier
+    work (the traces of its batch); waiting on it makes the current stream wait for the
+    collective, which is issued after the next batch's traces were enqueued and before the
+    buffer is reused (depth 2).
+    """
+
+    def __init__(self, rb: RowBands, device, frames_per_batch: int = 4, bpp: int = 3, depth: int = 2):
+        import torch
+        self.rb, self.F, self.bpp, self.depth = rb, max(1, frames_per_batch), bpp, depth
+        raw = max(1, rb.max_bands) * rb.band_rows * rb.width * bpp
+        self.slot_bytes = (raw + 255) // 256 * 256
+        self.rank_stride = self.F * self.slot_bytes
+        self.local = [torch.zeros(self.rank_stride, dtype=torch.uint8, device=device) for _ in range(depth)]
+        self.gathered = ([torch.empty(rb.world * self.rank_stride, dtype=torch.uint8, device=device)
+                          for _ in range(depth)] if rb.rank == 0 else [None] * depth)
+        self.k = 0          # frames rendered
+        self.batch = 0      # batches submitted
+        self.pending = None  # (work, buffer index, n_frames)
+
+    def frame_buffer(self) -> int:
+        b = self.local[self.batch % self.depth]
+        return b.data_ptr() + (self.k % self.F) * self.slot_bytes
+
+    def _submit(self, n_frames: int):
+        import torch.distributed as dist
+        i = self.batch % self.depth
+        n = n_frames * self.slot_bytes
+        # every rank gathers the same n bytes (the same frame count); rank 0's list points
+        # into its contiguous buffer at rank_stride intervals
+        send = self.local[i][:n]
+        glist = ([self.gathered[i][r * self.rank_stride:r * self.rank_stride + n] for r in range(self.rb.world)]
+                 if self.rb.rank == 0 else None)
+        work = dist.gather(send, glist, dst=0, async_op=True)
+        done = None
+        if self.pending is not None:
+            pw, pi, pn = self.pending
+            pw.wait()
+            done = (self.gathered[pi], pn)
+        self.pending = (work, i, n_frames)
+        self.batch += 1
+        return done
+
+    def commit(self):
+        self.k += 1
+        if self.k % self.F == 0:
+            return self._submit(self.F)
+        return None
+
+    def drain(self):
+        out = []
+        if self.k % self.F:
+            d = self._submit(self.k % self.F)
+            if d is not None:
+                out.append(d)
+            self.k += self.F - self.k % self.F  # next frame starts a fresh batch
+        if self.pending is not None:
+            pw, pi, pn = self.pending
+            pw.wait()
+            out.append((self.gathered[pi], pn))
+            self.pending = None
+        return out
