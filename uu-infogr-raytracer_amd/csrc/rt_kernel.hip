@@ -580,6 +580,22 @@ constexpr int HIT_NONE = 0x7fffffff;
 // Shading of one shaded hit (TraceSphere :847-873 / TracePlane :736-778): the colour is
 // accumulated in the reference's order -- mirror term (from the deeper segment `sec`),
 // then each light, then ambient.  Returns the colour; adds shadow rays to *n_shadow.
+// A light's shadow test can change the pixel only through I * att * phong vs 0 * phong.  When
+// every phong component is +-0 or NaN and I * att is finite, both give +-0 / NaN per
+// component (the sign of a zero never reaches a pixel: only additions, products, IEEE max and
+// the final clamp follow), so the test is skipped (RT_SHADOW_SKIP).  Ray counters are unchanged
+// (shadow rays = shaded diffuse hits x lights).
+#ifndef RT_SHADOW_SKIP
+#define RT_SHADOW_SKIP 1
+#endif
+__device__ __forceinline__ bool zero_or_nan(float v) { return !(v != 0.0f && v == v); }
+__device__ __forceinline__ bool shadow_matters(f3 ph, float intensity, float att) {
+    if constexpr (!RT_SHADOW_SKIP) return true;
+    const float ia = intensity * att;
+    const bool finite = __builtin_fabsf(ia) < __builtin_inff();
+    return !(finite && zero_or_nan(ph.x) && zero_or_nan(ph.y) && zero_or_nan(ph.z));
+}
+
 template <bool GPOW, int SMAX>
 __device__ __forceinline__ f3 shade_direct(const LaunchParams& p, bool is_sphere, int prim, f3 hp, f3 d, float t, f3 sec,
                                     unsigned* n_shadow) {
@@ -608,18 +624,7 @@ __device__ __forceinline__ f3 shade_direct(const LaunchParams& p, bool is_sphere
         for (int li = 0; li < p.L; ++li) {
             const DevLight& l = p.li[li];
             const bool l_ok = l.a2 > 0.0f && l.a2 < __builtin_inff();  // wave-uniform
-            bool blocked = false;
-            if constexpr (RT_ABLATE == 2) {
-                blocked = hp.x > 1e30f;
-            } else if constexpr (SMAX > 0) {
-                for_spheres<SMAX>(p.S, [&](int i) {
-                    if (!blocked) blocked = shadow_blocked(hp, l, l_ok, p.sph[i]);
-                });
-            } else {
-                for (int i = 0; i < p.S && !blocked; ++i) blocked = shadow_blocked(hp, l, l_ok, p.sph[i]);
-            }
-            const float inten = blocked ? 0.0f : l.intensity;
-            // ShapePhongShading, :665-695
+            // ShapePhongShading, :665-695 (first: it decides whether the shadow test matters)
             const f3 ldir = normalize(sub(mk(l.px, l.py, l.pz), hp));
             f3 ph = scale(kd, nmax0(dot(normal, ldir)));
             f3 spec = mk(0.0f, 0.0f, 0.0f);
@@ -629,6 +634,19 @@ __device__ __forceinline__ f3 shade_direct(const LaunchParams& p, bool is_sphere
                 spec = mul(mk(m.ks[0], m.ks[1], m.ks[2]), mk(sp, sp, sp));
             }
             ph = add(ph, spec);
+            bool blocked = false;
+            if (shadow_matters(ph, l.intensity, att)) {
+                if constexpr (RT_ABLATE == 2) {
+                    blocked = hp.x > 1e30f;
+                } else if constexpr (SMAX > 0) {
+                    for_spheres<SMAX>(p.S, [&](int i) {
+                        if (!blocked) blocked = shadow_blocked(hp, l, l_ok, p.sph[i]);
+                    });
+                } else {
+                    for (int i = 0; i < p.S && !blocked; ++i) blocked = shadow_blocked(hp, l, l_ok, p.sph[i]);
+                }
+            }
+            const float inten = blocked ? 0.0f : l.intensity;
             const float ia = inten * att;
             f3 term = mul(mk(ia, ia, ia), ph);
             if (!is_sphere) {
@@ -1120,33 +1138,7 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
             const DevLight& l = p.li[li];
             const f3 lp = mk(l.px, l.py, l.pz);
             const bool l_ok = l.a2 > 0.0f && l.a2 < __builtin_inff();  // wave-uniform
-#if RT_SHADOW_CULL
-            const ShadowBundle B = make_shadow_bundle(hp, l, diff);
-#else
-            Bundle B = make_bundle(hp, lp, diff, true);
-            B.ok = B.ok && l_ok && l.a >= 0x1p-40f && l.a <= 0x1p40f;
-#endif
-            const f3 hs = diff ? hp : B.O;  // idle lanes mirror a shading lane (results ignored)
-            bool blocked = !diff;
-            if constexpr (RT_CULLSTATS == 2) *n_shadow += (unsigned)((threadIdx.x & 63) == 0) << CNT_SHADOW_SHIFT;
-            for (int base = 0; RT_ABLATE != 2 && base < p.S; base += 64) {
-                const int n = min(64, p.S - base);
-#if RT_SHADOW_CULL
-                unsigned long long mk64 = shadow_cull_mask(p, B, l, base, n);
-#else
-                unsigned long long mk64 = cull_mask(p, B, base, n);
-#endif
-                while (mk64) {
-                    const int i = base + (int)__builtin_ctzll(mk64);
-                    mk64 &= mk64 - 1;
-                    if constexpr (RT_CULLSTATS == 1) *n_shadow += (unsigned)((threadIdx.x & 63) == 0) << CNT_SHADOW_SHIFT;
-                    blocked = blocked | shadow_blocked(hs, l, l_ok, p.sph[i]);  // no short-circuit branch
-                    if (__builtin_amdgcn_ballot_w64(!blocked) == 0) break;
-                }
-                if (__builtin_amdgcn_ballot_w64(!blocked) == 0) break;
-            }
-            const float inten = (blocked || !diff) ? 0.0f : l.intensity;
-            // ShapePhongShading, :665-695
+            // ShapePhongShading, :665-695 (first: it decides whether the shadow test matters)
             const f3 ldir = normalize(sub(lp, hp));
             f3 ph = scale(kd, nmax0(dot(normal, ldir)));
             f3 spec = mk(0.0f, 0.0f, 0.0f);
@@ -1156,6 +1148,36 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
                 spec = mul(mk(m.ks[0], m.ks[1], m.ks[2]), mk(sp, sp, sp));
             }
             ph = add(ph, spec);
+            const bool need = diff && shadow_matters(ph, l.intensity, att);
+            bool blocked = !need;
+            if (__builtin_amdgcn_ballot_w64(need) != 0) {  // some lane's pixel depends on this test
+
+#if RT_SHADOW_CULL
+                const ShadowBundle B = make_shadow_bundle(hp, l, need);
+#else
+                Bundle B = make_bundle(hp, lp, need, true);
+                B.ok = B.ok && l_ok && l.a >= 0x1p-40f && l.a <= 0x1p40f;
+#endif
+                const f3 hs = need ? hp : B.O;  // idle lanes mirror a shading lane (results ignored)
+                if constexpr (RT_CULLSTATS == 2) *n_shadow += (unsigned)((threadIdx.x & 63) == 0) << CNT_SHADOW_SHIFT;
+                for (int base = 0; RT_ABLATE != 2 && base < p.S; base += 64) {
+                    const int n = min(64, p.S - base);
+#if RT_SHADOW_CULL
+                    unsigned long long mk64 = shadow_cull_mask(p, B, l, base, n);
+#else
+                    unsigned long long mk64 = cull_mask(p, B, base, n);
+#endif
+                    while (mk64) {
+                        const int i = base + (int)__builtin_ctzll(mk64);
+                        mk64 &= mk64 - 1;
+                        if constexpr (RT_CULLSTATS == 1) *n_shadow += (unsigned)((threadIdx.x & 63) == 0) << CNT_SHADOW_SHIFT;
+                        blocked = blocked | shadow_blocked(hs, l, l_ok, p.sph[i]);  // no short-circuit branch
+                        if (__builtin_amdgcn_ballot_w64(!blocked) == 0) break;
+                    }
+                    if (__builtin_amdgcn_ballot_w64(!blocked) == 0) break;
+                }
+            }
+            const float inten = (!diff || (need && blocked)) ? 0.0f : l.intensity;
             const float ia = inten * att;
             f3 term = mul(mk(ia, ia, ia), ph);
             if (!is_sphere) {
