@@ -734,6 +734,40 @@ __device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d,
     return Hit{0.0f, HIT_NONE};
 }
 
+// Terminal segment (bounce count > limit): only its colour is used -- One iff a plane is
+// selected with t - 0.01 > 0 and no sphere beats it (TraceSecondaryRay :789-826 with the
+// terminal colours of TracePlane :734 / TraceSphere :843), otherwise Zero.  Planes first:
+// with no plane hit, or the nearest within 0.01, the colour is Zero whatever the spheres do,
+// so they are not tested (RT_TERMINAL).  Returns HIT_NONE (Zero) or the plane hit (One);
+// the walk classifies it exactly as it would the full nearest hit.
+#ifndef RT_TERMINAL
+#define RT_TERMINAL 1
+#endif
+template <int SMAX>
+__device__ __forceinline__ Hit terminal_direct(const LaunchParams& p, f3 o, f3 d) {
+    float best_p = __builtin_inff();
+    int win_p = -1;
+    for (int i = 0; i < p.P; ++i) {
+        const float t = plane_t(o, d, p.pl[i]);
+        if (t > 0.0f && t < best_p) {
+            best_p = t;
+            win_p = i;
+        }
+    }
+    if (win_p < 0 || !(best_p - 0.01f > 0.0f)) return Hit{0.0f, HIT_NONE};
+    const float a = dot(d, d);
+    const float a2 = 2.0f * a, a4 = 4.0f * a;
+    const bool a2_ok = a2 > 0.0f && a2 < __builtin_inff();
+    float best_s = __builtin_inff();
+    for_spheres<SMAX>(p.S, [&](int i) {
+        const float t = sphere_t(o, d, a2, a4, a2_ok, p.sph[i]);
+        const float tm = t - 0.01f;
+        if (tm > 0.0f && tm < best_s) best_s = t;
+    });
+    if (best_s < best_p) return Hit{0.0f, HIT_NONE};  // a sphere is selected: Zero
+    return Hit{best_p, ~win_p};
+}
+
 // DIRECT kernel: each lane walks its own chain with per-lane (divergent) control flow.
 template <int K, bool SCRATCH, bool GPOW, int SMAX>
 __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p) {
@@ -785,7 +819,8 @@ __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p
             o = reflect_at(p, o, d, h.t, h.prim);  // :854, CalculateReflectionRay :718-720
             ++count;
             ++cnt;
-            h = nearest_direct<false, SMAX>(p, o, d);
+            // count is the same for every lane still walking: no divergence here
+            h = (RT_TERMINAL && count > p.limit) ? terminal_direct<SMAX>(p, o, d) : nearest_direct<false, SMAX>(p, o, d);
         }
         // backward fold: every recorded hit is shaded in reverse order; a mirror hit
         // consumes the colour of the segment after it (levels 0..limit push at most one
@@ -1249,7 +1284,27 @@ __global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel(LaunchParams p
             }
         }
         if (__builtin_amdgcn_ballot_w64(active) == 0) break;
-        h = nearest_bundle<false>(p, o, d, active);
+        if (RT_TERMINAL && count + 1 > p.limit) {
+            // terminal segment (see terminal_direct): only lanes whose nearest plane lies beyond
+            // 0.01 need the spheres; the others are Zero
+            float best_p = __builtin_inff();
+            int win_p = -1;
+            for (int i = 0; i < p.P; ++i) {
+                const float t = plane_t(o, d, p.pl[i]);
+                if (t > 0.0f && t < best_p) {
+                    best_p = t;
+                    win_p = i;
+                }
+            }
+            const bool need = active && win_p >= 0 && best_p - 0.01f > 0.0f;
+            h = Hit{0.0f, HIT_NONE};
+            if (__builtin_amdgcn_ballot_w64(need) != 0) {
+                const Hit hn = nearest_bundle<false>(p, o, d, need);
+                if (need) h = hn;
+            }
+        } else {
+            h = nearest_bundle<false>(p, o, d, active);
+        }
     }
 
     // backward fold (converged): level by level from the deepest, every recorded hit is
