@@ -15,7 +15,8 @@ from collections import defaultdict
 
 def summarise(d, kernel="rtk::trace_"):
     vals = defaultdict(lambda: defaultdict(float))  # counter -> dispatch -> value
-    for fn in sorted(glob.glob(os.path.join(d, "p*", "*counter_collection.csv"))):
+    files = glob.glob(os.path.join(d, "p*", "*counter_collection.csv")) + glob.glob(os.path.join(d, "*counter_collection.csv"))
+    for fn in sorted(files):
         for row in csv.DictReader(open(fn)):
             if kernel not in row["Kernel_Name"]:
                 continue

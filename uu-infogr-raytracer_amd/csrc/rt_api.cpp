@@ -98,7 +98,7 @@ struct Device {
 
 struct SceneLayout {
     int S = 0, P = 0, L = 0, limit = 0;
-    size_t off_sph = 0, off_mat = 0, off_pl = 0, off_li = 0, off_cull = 0, bytes = 0;
+    size_t off_sph = 0, off_mat = 0, off_pl = 0, off_li = 0, off_cull = 0, off_shc = 0, bytes = 0;
     bool generic_pow = false;        // a specular material with n not in {0.5, 1, 2}
     std::vector<DevSphere> host_sph;  // for the per-frame primary constants
 };
@@ -325,6 +325,7 @@ void scene_params(const rt_ctx* ctx, const Device& d, LaunchParams& lp) {
     lp.pl = (const DevPlane*)(base + L.off_pl);
     lp.li = (const DevLight*)(base + L.off_li);
     lp.scull = (const DevSphereCull*)(base + L.off_cull);
+    lp.shc = (const DevShadowCull*)(base + L.off_shc);
     lp.S = L.S, lp.P = L.P, lp.L = L.L, lp.limit = L.limit;
     lp.counters = d.d_counters;
 }
@@ -520,7 +521,8 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
     L.off_pl = al(L.off_mat + sizeof(DevMaterial) * (size_t)(n_spheres + n_planes));
     L.off_li = al(L.off_pl + sizeof(DevPlane) * (size_t)n_planes);
     L.off_cull = al(L.off_li + sizeof(DevLight) * (size_t)n_lights);
-    L.bytes = al(L.off_cull + sizeof(DevSphereCull) * (size_t)n_spheres) + 256;
+    L.off_shc = al(L.off_cull + sizeof(DevSphereCull) * (size_t)n_spheres);
+    L.bytes = al(L.off_shc + sizeof(DevShadowCull) * (size_t)n_spheres * (size_t)n_lights) + 256;
 
     std::vector<unsigned char> blob(L.bytes, 0);
     DevSphere* sph = (DevSphere*)(blob.data() + L.off_sph);
@@ -528,6 +530,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
     DevPlane* pl = (DevPlane*)(blob.data() + L.off_pl);
     DevLight* li = (DevLight*)(blob.data() + L.off_li);
     DevSphereCull* cull = (DevSphereCull*)(blob.data() + L.off_cull);
+    DevShadowCull* shc = (DevShadowCull*)(blob.data() + L.off_shc);
     for (int i = 0; i < n_spheres; ++i) {
         const rt_sphere& s = spheres[i];
         sph[i] = DevSphere{s.center.x, s.center.y, s.center.z, s.radius * s.radius};  // :336
@@ -574,7 +577,20 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
         d.ax = (float)A[0], d.ay = (float)A[1], d.az = (float)A[2];
         d.ux = (float)U[0], d.uy = (float)U[1], d.uz = (float)U[2];
         d.vx = (float)V[0], d.vy = (float)V[1], d.vz = (float)V[2];
+        d.lane_cull = (d.a >= 0x1p-40f && d.a <= 0x1p40f && std::isfinite(d.a2)) ? 1u : 0u;
         li[i] = d;
+        // per-lane shadow cull records (see DevShadowCull): centre in the light's frame,
+        // threshold base rounded up; spheres outside the analysed range are never culled
+        for (int k = 0; k < n_spheres; ++k) {
+            const DevSphere& s = sph[k];
+            const double cn = std::fabs((double)s.cx) + std::fabs((double)s.cy) + std::fabs((double)s.cz);
+            const double cu = (double)s.cx * d.ux + (double)s.cy * d.uy + (double)s.cz * d.uz;
+            const double cv = (double)s.cx * d.vx + (double)s.cy * d.vy + (double)s.cz * d.vz;
+            float t0 = INFINITY;
+            if (cull[k].rr >= 0x1p-50f && cull[k].rr < 0x1p40f && cn < 0x1p40 && std::isfinite(cu) && std::isfinite(cv))
+                t0 = std::nextafter((float)((double)cull[k].rr + 0x1p-8 * cn * (1.0 + 0x1p-20)), INFINITY);
+            shc[(size_t)i * n_spheres + k] = DevShadowCull{(float)cu, (float)cv, t0, 0.0f};
+        }
     }
     for (int i = 0; i < n_spheres + n_planes; ++i)
         if ((mat[i].flags & MAT_SPEC) && mat[i].pow_kind == POW_GENERIC) L.generic_pow = true;

@@ -47,7 +47,7 @@ struct DevLight {
     float a;      // dot(p, p)       : IntersectsSphere's `a` for a shadow ray (dir = position)
     float a2;     // 2 * a
     float a4;     // 4 * a
-    float pad;
+    uint32_t lane_cull;  // 1: the per-lane shadow cull may be used (a in [2^-40, 2^40], 2a finite)
     // shadow-cull frame (culling only, never in a result): A ~ p/|p| (every shadow ray of this
     // light has direction p), U, V ~ orthonormal to A
     float ax, ay, az, pad1;
@@ -58,6 +58,15 @@ struct DevLight {
 // Per-sphere culling record: centre and a radius bound r' >= sqrt(r^2) * (1 + 2^-8).
 struct DevSphereCull {
     float cx, cy, cz, rr;
+};
+
+// Per-(light, sphere) record of the direct kernel's per-lane shadow cull [L][S]: the
+// sphere centre in the light's frame (cu = C.U, cv = C.V) and the threshold base
+// t0 >= r' + 2^-8 |C|_1 (rounded up; +inf when the sphere may not be culled).  A shadow
+// ray from hp skips sphere i when (cu - hp.U)^2 + (cv - hp.V)^2 > (t0 + 2^-8 |hp|_1)^2
+// (culling only; rt_kernel.hip, shadow_lane_cull, for why this is exact).
+struct DevShadowCull {
+    float cu, cv, t0, pad;
 };
 
 // Work counters: each workgroup adds its totals into slot (block id % COUNTER_SLOTS) so that
@@ -94,6 +103,7 @@ struct LaunchParams {
     const DevPlane* pl;
     const DevLight* li;
     const DevSphereCull* scull;  // [S]
+    const DevShadowCull* shc;    // [L][S]
     const float* lxt;  // [W]: ((float)x / W - 0.5f) * pw, TracePixel :963-965
     const float* lyt;  // [H]: ((float)y / H - 0.5f) * ph
     int S, P, L, limit;

@@ -23,7 +23,15 @@
 //    skipped (sqrt/divisions of spheres behind the ray, the far root) -- see root_t1.
 #include <hip/hip_runtime.h>
 
+#include "rt_fastmath.h"
 #include "rt_internal.h"
+
+// RT_FASTMATH 1 (shipped): correctly rounded sqrt / reciprocal / division through the short
+// sequences of rt_fastmath.h inside their verified domains (same bits as the generic
+// operations for every input, tools/fastmath_check.hip); 0 = the generic sequences.
+#ifndef RT_FASTMATH
+#define RT_FASTMATH 1
+#endif
 
 // RT_ABLATE (timing experiments only, tools/ab.py; never defined in the shipped build):
 //   1 = no shading (fold skipped), 2 = no shadow rays, 3 = primary segment only.
@@ -50,6 +58,33 @@ constexpr int WG_WX = RT_WG_WX, WG_WY = RT_WG_WY, WG_WAVES = WG_WX * WG_WY, WG_T
 
 namespace rtk {
 
+// Correctly rounded binary32 operations (bit-identical either way, see rt_fastmath.h).
+// RT_FASTMATH bits: 1 = normalize's 1/sqrt, 2 = other sqrt, 4 = reciprocal / division.
+__device__ __forceinline__ float cr_sqrt(float x) {
+    if constexpr ((RT_FASTMATH & 2) != 0) return sqrt_cr(x);
+    else return __builtin_sqrtf(x);
+}
+__device__ __forceinline__ float cr_inv_len(float x) {  // 1f / MathF.Sqrt(x)
+    if constexpr ((RT_FASTMATH & 1) != 0) return inv_len_cr(x);
+    else return 1.0f / __builtin_sqrtf(x);
+}
+__device__ __forceinline__ float cr_rcp(float x) {
+    if constexpr ((RT_FASTMATH & 4) != 0) return rcp_cr(x);
+    else return 1.0f / x;
+}
+// a / b where the quotient is used only when `need` (the generic fallback runs only there).
+__device__ __forceinline__ float cr_div_if(bool need, float a, float b) {
+    if constexpr ((RT_FASTMATH & 4) != 0) {
+        float q = div_cr_fast(a, b);
+        if (__builtin_expect(need && !(fm_in(a, FM_DIV_LO, FM_DIV_HI) && fm_in(b, FM_DIV_LO, FM_DIV_HI)), 0))
+            q = a / b;
+        return q;
+    } else {
+        (void)need;
+        return a / b;
+    }
+}
+
 struct f3 {
     float x, y, z;
 };
@@ -63,7 +98,7 @@ __device__ __forceinline__ f3 scale(f3 a, float s) { return mk(a.x * s, a.y * s,
 __device__ __forceinline__ float dot(f3 a, f3 b) { return ((a.x * b.x) + (a.y * b.y)) + (a.z * b.z); }
 // Vector3.Normalize: s = 1f / MathF.Sqrt(x*x + y*y + z*z); v * s
 __device__ __forceinline__ f3 normalize(f3 a) {
-    float s = 1.0f / __builtin_sqrtf(dot(a, a));
+    const float s = cr_inv_len(dot(a, a));
     return scale(a, s);
 }
 // Math.Max(x, 0f) / Math.Min(a, b) on .NET Core 3.0+: IEEE 754-2019 maximum / minimum
@@ -86,7 +121,7 @@ template <bool GPOW>
 __device__ __forceinline__ float spec_pow(float x, const DevMaterial& m) {
     switch (m.pow_kind) {
         case POW_ONE: return x;
-        case POW_HALF: return __builtin_sqrtf(x);
+        case POW_HALF: return cr_sqrt(x);
         case POW_TWO: return x * x;
         default:
             if constexpr (GPOW) return (float)pow((double)x, (double)m.n);
@@ -111,10 +146,11 @@ __device__ __forceinline__ float spec_pow(float x, const DevMaterial& m) {
 __device__ __forceinline__ float root_t1(float b, float disc, float a2) {
     float t = 0.0f;
     if (disc >= 0.0f && b < 0.0f) {
-        const float sq = __builtin_sqrtf(disc);  // == (float)Math.Sqrt((double)disc)
+        const float sq = cr_sqrt(disc);  // == (float)Math.Sqrt((double)disc)
         const float nb = -b;
-        const float q = (nb - sq) / a2;  // predicated, not branched: one exec-mask region less
-        t = nb > sq ? q : 0.0f;
+        const bool sel = nb > sq;
+        const float q = cr_div_if(sel, nb - sq, a2);  // predicated, not branched
+        t = sel ? q : 0.0f;
     }
     return t;
 }
@@ -151,9 +187,10 @@ __device__ __forceinline__ bool shadow_blocked(f3 hp, const DevLight& l, bool a2
     if (a2_ok) {
         bool hit = false;
         if (disc >= 0.0f && b < 0.0f) {
-            const float sq = __builtin_sqrtf(disc);
+            const float sq = cr_sqrt(disc);
             const float nb = -b;
-            hit = (nb > sq) & ((nb - sq) / l.a2 - 0.001f > 0.0f);
+            const bool sel = nb > sq;
+            hit = sel & (cr_div_if(sel, nb - sq, l.a2) - 0.001f > 0.0f);
         }
         return hit;
     }
@@ -172,7 +209,9 @@ __device__ __forceinline__ bool shadow_blocked(f3 hp, const DevLight& l, bool a2
 __device__ __forceinline__ float plane_t(f3 o, f3 d, const DevPlane& p) {
     const float num = ((-o.x * p.nx - o.y * p.ny) - o.z * p.nz) + p.cn;
     const float den = dot(d, mk(p.nx, p.ny, p.nz));
-    return ((num > 0.0f && den > 0.0f) || (num < 0.0f && den < 0.0f)) ? num / den : 0.0f;
+    const bool sel = (num > 0.0f && den > 0.0f) || (num < 0.0f && den < 0.0f);
+    const float q = cr_div_if(sel, num, den);
+    return sel ? q : 0.0f;
 }
 
 // ShiftColor, :1046-1052: Math.Clamp (NaN passes), * 255f, Math.Floor, (int), (byte).
@@ -596,6 +635,41 @@ __device__ __forceinline__ bool shadow_matters(f3 ph, float intensity, float att
     return !(finite && zero_or_nan(ph.x) && zero_or_nan(ph.y) && zero_or_nan(ph.z));
 }
 
+// Per-lane shadow cull of the direct kernel (RT_LANE_SHADOW_CULL).  Every shadow ray of light
+// l has direction p_l (Q2), so sphere i can block the ray from hp only if the line
+// {hp + s p_l} passes within r of its centre C: in the light's host-built frame (U, V ~ unit,
+// orthogonal to A ~ p_l/|p_l|) that distance is D = |((C - hp).U, (C - hp).V)|.  The host
+// stores cu = C.U, cv = C.V and t0 >= r' + 2^-8 |C|_1 (r' >= r (1 + 2^-8)); the lane skips
+// the exact test when (cu - hp.U)^2 + (cv - hp.V)^2 > (t0 + 2^-8 |hp|_1)^2.
+// Exactness: with u = hp - C and N = |C|_1 + |hp|_1 >= |u|, the binary32 discriminant of
+// IntersectsSphere is negative whenever D >= r (1 + 3 eps) + 9.2e-4 |u| (the error analysis
+// of cull_mask, invariant in the scale of the direction; a in [2^-40, 2^40], |u| < 2^41, so
+// nothing overflows and, since a culled sphere has D > t0 >= 2^-25, nothing underflows),
+// and disc < 0 makes shadow_blocked false in both of its branches.  The rounding of the
+// cull arithmetic (cu, cv rounded from binary64, hp.U and hp.V in binary32, the frame's own
+// rounding) perturbs D by less than 2^-20 N, so a cull implies D > r (1 + 2^-8) + 2^-9 N,
+// twice the 9.2e-4 |u| needed.  NaN / inf anywhere, |hp|_1 >= 2^40, or a sphere the host
+// excluded (t0 = +inf) fail the comparison: the exact test runs.
+#ifndef RT_LANE_SHADOW_CULL
+#define RT_LANE_SHADOW_CULL 0
+#endif
+struct LaneShadowCull {
+    float hu, hv, m;
+};
+__device__ __forceinline__ LaneShadowCull lane_shadow_frame(f3 hp, const DevLight& l) {
+    LaneShadowCull c;
+    c.hu = dot(hp, mk(l.ux, l.uy, l.uz));
+    c.hv = dot(hp, mk(l.vx, l.vy, l.vz));
+    const float hn = __builtin_fabsf(hp.x) + __builtin_fabsf(hp.y) + __builtin_fabsf(hp.z);
+    c.m = hn < 0x1p40f ? hn * 0x1.004p-8f : __builtin_inff();  // >= 2^-8 |hp|_1
+    return c;
+}
+__device__ __forceinline__ bool lane_shadow_far(const LaneShadowCull& c, const DevShadowCull& s) {
+    const float du = s.cu - c.hu, dv = s.cv - c.hv;
+    const float t = s.t0 + c.m;
+    return __builtin_fmaf(du, du, dv * dv) > t * t;
+}
+
 template <bool GPOW, int SMAX>
 __device__ __forceinline__ f3 shade_direct(const LaunchParams& p, bool is_sphere, int prim, f3 hp, f3 d, float t, f3 sec,
                                     unsigned* n_shadow) {
@@ -619,7 +693,7 @@ __device__ __forceinline__ f3 shade_direct(const LaunchParams& p, bool is_sphere
     if (flags & MAT_DIFFUSE) {
         const f3 view = normalize(d);  // ShapePhongShading :668 (not negated)
         // sphere: (1 / t) * t (:866);  plane: (float)(1 / Math.Pow(t, 2)) (:754), exact as 1/(t*t) in f64
-        const float att = is_sphere ? (1.0f / t) * t : (float)(1.0 / ((double)t * (double)t));
+        const float att = is_sphere ? cr_rcp(t) * t : (float)(1.0 / ((double)t * (double)t));
         const f3 kd = mk(m.kd[0], m.kd[1], m.kd[2]);
         for (int li = 0; li < p.L; ++li) {
             const DevLight& l = p.li[li];
@@ -642,6 +716,11 @@ __device__ __forceinline__ f3 shade_direct(const LaunchParams& p, bool is_sphere
                     for_spheres<SMAX>(p.S, [&](int i) {
                         if (!blocked) blocked = shadow_blocked(hp, l, l_ok, p.sph[i]);
                     });
+                } else if (RT_LANE_SHADOW_CULL && l.lane_cull) {  // wave-uniform
+                    const LaneShadowCull c = lane_shadow_frame(hp, l);
+                    const DevShadowCull* sc = p.shc + li * p.S;
+                    for (int i = 0; i < p.S && !blocked; ++i)
+                        if (!lane_shadow_far(c, sc[i])) blocked = shadow_blocked(hp, l, l_ok, p.sph[i]);
                 } else {
                     for (int i = 0; i < p.S && !blocked; ++i) blocked = shadow_blocked(hp, l, l_ok, p.sph[i]);
                 }
@@ -1167,7 +1246,7 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
     if (__builtin_amdgcn_ballot_w64(diff) != 0) {
         const f3 view = normalize(d);  // ShapePhongShading :668 (not negated)
         // sphere: (1 / t) * t (:866);  plane: (float)(1 / Math.Pow(t, 2)) (:754), exact as 1/(t*t) in f64
-        const float att = is_sphere ? (1.0f / t) * t : (float)(1.0 / ((double)t * (double)t));
+        const float att = is_sphere ? cr_rcp(t) * t : (float)(1.0 / ((double)t * (double)t));
         const f3 kd = mk(m.kd[0], m.kd[1], m.kd[2]);
         for (int li = 0; li < p.L; ++li) {
             const DevLight& l = p.li[li];
