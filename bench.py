@@ -46,8 +46,9 @@ def parse():
                     help="N>1: gather each frame before tracing the next (no double buffering)")
     ap.add_argument("--batch", type=int, default=8,
                     help="N>1: frames per RCCL gather (double-buffered; 1 = one gather per frame)")
-    ap.add_argument("--band-format", choices=["rgb24", "int32"], default="rgb24",
-                    help="N>1: band sets shipped to rank 0 as packed 24-bit RGB or int32 pixels")
+    ap.add_argument("--band-format", choices=["tiles", "rgb24", "int32"], default="tiles",
+                    help="N>1: band sets shipped to rank 0 tile-encoded (lossless, rt_encode_bands), as packed "
+                         "24-bit RGB or as int32 pixels")
     ap.add_argument("--dist-path", action="store_true",
                     help="rehearsal: run the N>1 band/gather path even with one process (RCCL world of 1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -136,6 +137,7 @@ def main():
         pass
 
     streams = [stream]
+    tg = None  # tile-encoded gather (N > 1, --band-format tiles)
     if not distributed:
         nf = max(1, args.inflight)
         frames = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in range(nf)]
@@ -161,12 +163,53 @@ def main():
                     ctx.scatter_bands(W, H, rb.band_rows, r, world, parts[r].data_ptr(), frame.data_ptr(), s)
 
         if args.no_pipeline:
+            if args.band_format == "tiles":
+                raise SystemExit("--no-pipeline ships raw band sets: use --band-format int32/rgb24")
             bg = BandGather(rb, torch.device("cuda", local))
 
             def step():
                 # trace this rank's bands -> RCCL gather of the slots to rank 0 -> reassemble there
                 ctx.render_bands(W, H, rb.band_rows, rank, world, bg.local.data_ptr(), s)
                 scatter(bg.gather())
+        elif args.band_format == "tiles":
+            from raytracer_hip import wire_layout
+            from raytracer_hip.dist import TileBandGather
+
+            def t_encode(raw, n, wire, size, st):
+                ctx.encode_bands(W, H, rb.band_rows, rank, world, raw.data_ptr(), rb.slot_elems, n, wire.data_ptr(),
+                                 size.data_ptr(), st.cuda_stream)
+
+            def t_decode(recv, rank_stride, n, frames_, st):
+                ctx.decode_gathered(W, H, rb.band_rows, world, recv.data_ptr(), rank_stride, n, frames_.data_ptr(),
+                                    W * H, st.cuda_stream)
+
+            tg = TileBandGather(rb, torch.device("cuda", local), args.batch,
+                                lambda n: wire_layout(W, H, rb.band_rows, world, n), t_encode, t_decode)
+            # frames alternate between trace streams (two in flight per rank); at a batch end the
+            # encode runs on `stream` after the others joined it, and the trace streams then wait
+            # for it (the next-but-one batch reuses the raw buffer); collectives are waited on
+            # the gather's own side streams, never on a trace stream
+            tstreams = [stream] + [torch.cuda.Stream() for _ in range(max(1, args.inflight) - 1)]
+
+            def step():
+                k = tg.k
+                ctx.render_bands_ex(W, H, rb.band_rows, rank, world, tg.raw_frame().data_ptr(), abi.RT_BANDS_INT32,
+                                    tstreams[k % len(tstreams)].cuda_stream)
+                end = (k + 1) % tg.F == 0
+                if end:
+                    for t in tstreams[1:]:
+                        stream.wait_stream(t)
+                tg.commit(stream)
+                if end:
+                    for t in tstreams[1:]:
+                        t.wait_stream(stream)
+
+            def finish():  # noqa: F811  -- the last (possibly partial) batch, every stage
+                for t in tstreams[1:]:
+                    stream.wait_stream(t)
+                tg.drain(stream)
+                stream.wait_stream(tg.comm)
+                stream.wait_stream(tg.dec)
         else:
             fmt = abi.RT_BANDS_RGB24 if args.band_format == "rgb24" else abi.RT_BANDS_INT32
             bgb = BatchedBandGather(rb, torch.device("cuda", local), frames_per_batch=args.batch,
@@ -216,6 +259,8 @@ def main():
     finish()
     torch.cuda.synchronize()
     ctx.reset_stats()
+    if tg is not None:
+        tg.bytes_sent = 0
 
     if distributed:
         dist.barrier()
@@ -317,6 +362,10 @@ def main():
             },
             "cpu_baseline": None,
         }
+        if tg is not None:
+            # wire bytes each rank shipped per frame (max over ranks, as gathered), vs the raw band set
+            out["config"]["gather_wire_bytes_per_frame"] = tg.bytes_sent / steps
+            out["config"]["gather_rgb24_bytes_per_frame"] = 3 * rb.slot_elems
         if world == 1:
             # Tick() path for context: full frame into pinned host memory (PCIe D2H included); not `value`
             import numpy as np

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 3
+#define RT_ABI_VERSION 4
 
 /* ---- status codes ---------------------------------------------------------- */
 enum {
@@ -209,6 +209,35 @@ int rt_render_bands_ex(rt_ctx* ctx, int width, int height, int band_rows, int ba
 int rt_scatter_gathered(rt_ctx* ctx, int width, int height, int band_rows, int world,
                         const void* d_gathered, size_t slot_bytes, int format, int32_t* d_frame,
                         void* hip_stream);
+
+/* ---- tile codec for the gather to rank 0 (ABI 4) ------------------
+ * Lossless: each rank encodes its int32 band sets (as rt_render_bands writes them, the
+ * slot of the largest band set per frame) into a "wire" -- per 8x8 tile a raw first pixel,
+ * left/above prediction, zigzag residuals as w-bit planes (one wave ballot each) -- and rank
+ * 0 decodes all ranks' wires straight into the frames.  Rendered frames are mostly flat, so
+ * the wire is ~7-11x smaller than RGB24 at 1080p; the format is specified
+ * in raytracer_hip/tilecodec.py.  The wire's size varies: the fixed part (header, tile
+ * headers, chunk bases) is the same on every rank, the payload follows it. */
+typedef struct rt_wire_layout {
+    uint64_t fixed_bytes;  /* header + tile headers + chunk bases (8-aligned)          */
+    uint64_t max_bytes;    /* fixed_bytes + the largest possible payload (capacity)     */
+    int32_t tiles_x, tiles_y, tiles_per_frame, n_frames, n_tiles, n_chunks;
+} rt_wire_layout;
+/* Sizes of one rank's wire for n_frames frames (the same for every rank of `world`). */
+int rt_wire_layout_of(int width, int height, int band_rows, int world, int n_frames, rt_wire_layout* out);
+/* Encode n_frames band sets of `rank` (frame f at d_bands + f * frame_stride int32, each
+ * at least the largest band set: bands_of(height, band_rows, 0, world) * band_rows * width)
+ * into d_wire (8-aligned, max_bytes capacity).  *d_wire_bytes (device int64, may be NULL)
+ * receives the wire's size in bytes.  Three launches, asynchronous on hip_stream. */
+int rt_encode_bands(rt_ctx* ctx, int width, int height, int band_rows, int rank, int world,
+                    const int32_t* d_bands, size_t frame_stride, int n_frames, void* d_wire,
+                    int64_t* d_wire_bytes, void* hip_stream);
+/* Decode the wires of all `world` ranks (rank r's at d_gathered + r * rank_stride, 8-aligned)
+ * into frame f = d_frames + f * frame_stride (int32, row-major) for f < n_frames.  One
+ * launch, asynchronous on hip_stream. */
+int rt_decode_gathered(rt_ctx* ctx, int width, int height, int band_rows, int world,
+                       const void* d_gathered, size_t rank_stride, int n_frames, int32_t* d_frames,
+                       size_t frame_stride, void* hip_stream);
 
 /* ---- double-buffered frames ------------------------------ */
 /* Asynchronous Tick(): captures the current camera, enqueues the trace and the D2H copy

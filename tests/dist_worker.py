@@ -154,3 +154,70 @@ def run_batched(rank, world, port, cfg, width, height, band_rows, frames, per_ba
         dist.barrier()
     finally:
         dist.destroy_process_group()
+
+
+def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batch, result_path):
+    """bench.py's default N>1 step: F frames per batch, tile-encoded band sets (host mirror of
+    rt_encode_bands), size all_reduce + gather, rank 0 decodes every frame (host mirror of
+    rt_decode_gathered) and checks it against the oracle."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path[:0] = [os.path.join(root, "uu-infogr-raytracer_amd"), os.path.join(root, "oracle"), here]
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import pyoracle
+    from raytracer_hip import scenes, tilecodec
+    from raytracer_hip.dist import RowBands, TileBandGather
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        base = scenes.config(cfg).resized(width, height)
+
+        def scene_for(k):
+            sc = base.resized(width, height)
+            sc.camera = ((0.0, 0.0, 0.0), 0.04 * k - 0.1, -0.02 * k)
+            return sc
+
+        rb = RowBands(width, height, band_rows, rank, world)
+        got = {}
+        batch_of = []  # frame index of every decoded frame slot, in decode order
+
+        def encode(raw, n, wire, size, _stream):
+            b = tilecodec.encode(raw.numpy()[:n * rb.slot_elems], width, height, band_rows, rank, world, n)
+            wire.numpy()[:len(b)] = np.frombuffer(b, dtype=np.uint8)
+            size[0] = len(b)
+
+        decoded = [0]
+
+        def decode(recv, rank_stride, n, frames_, _stream):
+            host = recv.numpy()
+            fr = frames_.numpy().reshape(-1, height, width)
+            fr[:] = -7
+            for r in range(world):
+                tilecodec.decode_into(fr[:n], host[r * rank_stride:(r + 1) * rank_stride], width, height,
+                                      band_rows, r, world)
+            for f in range(n):
+                got[decoded[0] + f] = fr[f].copy()
+            decoded[0] += n
+
+        g = TileBandGather(rb, "cpu", per_batch, lambda n: tilecodec.layout(width, height, band_rows, world, n),
+                           encode, decode)
+        for k in range(frames):
+            raw = g.raw_frame().numpy()
+            raw[:] = 0x5A5A5A  # rows this rank does not own must not leak into the frame
+            for l0, y0, n in rb.row_spans():
+                rows, _ = pyoracle.render(scene_for(k), pyoracle.MODE_NEAREST, 2, rows=(y0, y0 + n))
+                raw[l0 * width:(l0 + n) * width] = rows.reshape(-1)
+            g.commit()
+        g.drain()
+        if rank == 0:
+            bad = [k for k in range(frames)
+                   if k not in got or not np.array_equal(got[k], pyoracle.render(scene_for(k), pyoracle.MODE_NEAREST, 2)[0])]
+            with open(result_path, "w") as f:
+                f.write("ok" if not bad else f"bad frames {bad} of {len(got)}")
+        dist.barrier()
+    finally:
+        dist.destroy_process_group()

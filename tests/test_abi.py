@@ -56,7 +56,7 @@ def test_struct_layouts_match_header():
 
 
 def test_abi_version(rtlib):
-    assert rtlib.rt_abi_version() == 3 == abi.RT_ABI_VERSION
+    assert rtlib.rt_abi_version() == 4 == abi.RT_ABI_VERSION
     hdr = open(HEADER).read()
     assert re.search(r"#define RT_ABI_VERSION (\d+)", hdr).group(1) == str(abi.RT_ABI_VERSION)
 
@@ -182,7 +182,7 @@ def test_ctypes_layouts_match_the_c_header(tmp_path):
     ctypes mirror (what the C#/Go/Python bindings must reproduce)."""
     import subprocess
     structs = {n: getattr(abi, n) for n in ("rt_vec3", "rt_material", "rt_sphere", "rt_plane", "rt_light",
-                                           "rt_camera", "rt_view", "rt_segment", "rt_stats")}
+                                           "rt_camera", "rt_view", "rt_segment", "rt_stats", "rt_wire_layout")}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "raytracer_hip.h"', "int main(void) {"]
     for n, t in structs.items():
         lines.append(f'printf("{n} %zu\\n", sizeof({n}));')

@@ -124,3 +124,25 @@ def test_scatter_gathered_host_matches_scatter_host():
                 b = pack_rgb24(rows) if bpp == 3 else rows.astype(np.int32).view(np.uint8).reshape(-1)
                 buf[r * stride + l0 * W * bpp:r * stride + l0 * W * bpp + b.size] = b
         assert np.array_equal(scatter_gathered_host(buf, stride, W, H, br, world, bpp), frame)
+
+
+@pytest.mark.parametrize("world,frames,per_batch", [(2, 7, 3), (3, 5, 2), (2, 9, 2)])
+def test_gloo_tile_encoded_gather(tmp_path, world, frames, per_batch):
+    """bench.py's default N>1 step: tile-encoded band sets, size all_reduce + gather, three-stage
+    pipeline; every frame decodes to its own oracle frame, the last batch may be partial."""
+    import dist_worker
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    result = tmp_path / "result.txt"
+    procs = [ctx.Process(target=dist_worker.run_tiles,
+                         args=(r, world, port, "C3", 43, 29, 4, frames, per_batch, str(result))) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0] * world, codes
+    assert result.read_text() == "ok"

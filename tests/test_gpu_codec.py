@@ -1,0 +1,114 @@
+"""GPU parity of the tile codec kernels (rt_encode_bands / rt_decode_gathered, csrc/rt_codec.hip):
+the device wire equals the host mirror's bytes (tilecodec.py) exactly -- the layout is
+deterministic -- and decoding every rank's wire reproduces the frame bit for bit, from
+synthetic images and from the trace kernel's own band sets."""
+import os
+
+import numpy as np
+import pytest
+
+from raytracer_hip import scenes
+from raytracer_hip import tilecodec as tc
+from raytracer_hip.dist import RowBands
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _frames(kind, F, H, W, seed=0):
+    rng = np.random.default_rng(seed)
+    if kind == "noise":
+        return rng.integers(0, 1 << 24, size=(F, H, W)).astype(np.int32)
+    if kind == "flat":
+        return np.full((F, H, W), 0x2B2B2B, dtype=np.int32)
+    if kind == "golden":
+        img = np.load(os.path.join(GOLDEN, "frame_C3_96x54.npy")).astype(np.int32)
+        img = np.tile(img, (-(-H // img.shape[0]), -(-W // img.shape[1])))[:H, :W]
+        return np.stack([np.roll(img, 3 * f, axis=1) for f in range(F)])
+    base = (np.add.outer(np.arange(H) * 3, np.arange(W)) & 255)
+    return np.stack([((base + f) * 0x010101 + rng.integers(0, 3, size=(H, W))) & 0xFFFFFF
+                     for f in range(F)]).astype(np.int32)
+
+
+def _band_set(frames, band_rows, rank, world):
+    F, H, W = frames.shape
+    rb = RowBands(W, H, band_rows, rank, world)
+    s = np.full((F, rb.slot_elems // W, W), 0x7E5A3C, dtype=np.int32)  # unused rows: garbage
+    for l0, y0, n in rb.row_spans():
+        s[:, l0:l0 + n] = frames[:, y0:y0 + n]
+    return rb, s.reshape(-1)
+
+
+@pytest.mark.parametrize("kind", ["golden", "smooth", "noise", "flat"])
+@pytest.mark.parametrize("W,H,band_rows,world,F", [(96, 54, 8, 2, 1), (100, 37, 4, 3, 3), (1, 1, 8, 1, 1),
+                                                   (33, 65, 5, 8, 2), (257, 130, 8, 1, 2), (64, 16, 8, 4, 5)])
+def test_device_wire_equals_host_mirror_and_decodes(gpu_ctx, kind, W, H, band_rows, world, F):
+    import torch
+    frames = _frames(kind, F, H, W, seed=W + H + F)
+    lay = tc.layout(W, H, band_rows, world, F)
+    stride = (lay.max_bytes + 255) // 256 * 256
+    gathered = torch.zeros(world * stride, dtype=torch.uint8, device="cuda")
+    size = torch.zeros(1, dtype=torch.int64, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    for r in range(world):
+        rb, bs = _band_set(frames, band_rows, r, world)
+        d_bs = torch.from_numpy(bs).cuda()
+        wire = gathered[r * stride:(r + 1) * stride]
+        wire.fill_(0xCD)
+        gpu_ctx.encode_bands(W, H, band_rows, r, world, d_bs.data_ptr(), rb.slot_elems, F, wire.data_ptr(),
+                             size.data_ptr(), s)
+        torch.cuda.synchronize()
+        want = tc.encode(bs, W, H, band_rows, r, world, F)
+        assert int(size.item()) == len(want)
+        got = wire[:len(want)].cpu().numpy().tobytes()
+        assert got == want, f"rank {r}: wire differs from the host mirror"
+    out = torch.full((F * H * W,), -1, dtype=torch.int32, device="cuda")
+    gpu_ctx.decode_gathered(W, H, band_rows, world, gathered.data_ptr(), stride, F, out.data_ptr(), H * W, s)
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy().reshape(F, H, W), frames)
+
+
+@pytest.mark.parametrize("cfg,world,band_rows", [("C2", 2, 8), ("C3", 8, 8), ("C4", 3, 8), ("REF", 5, 4)])
+def test_traced_band_sets_roundtrip_to_the_frame(gpu_ctx, cfg, world, band_rows):
+    """The N>1 data path on one GPU: every simulated rank traces its band set (rt_render_bands),
+    encodes it, rank 0 decodes all wires -> identical to the single-launch frame."""
+    import torch
+    from raytracer_hip import abi
+    sc = scenes.config(cfg)
+    if cfg != "C2":
+        sc = sc.resized(640, 360)
+    W, H = sc.width, sc.height
+    gpu_ctx.set_scene(sc)
+    full = gpu_ctx.render(W, H).copy()
+    lay = tc.layout(W, H, band_rows, world, 1)
+    stride = (lay.max_bytes + 255) // 256 * 256
+    gathered = torch.zeros(world * stride, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    total = 0
+    for r in range(world):
+        rb = RowBands(W, H, band_rows, r, world)
+        buf = torch.zeros(rb.slot_elems, dtype=torch.int32, device="cuda")
+        gpu_ctx.render_bands_ex(W, H, band_rows, r, world, buf.data_ptr(), abi.RT_BANDS_INT32, s)
+        size = torch.zeros(1, dtype=torch.int64, device="cuda")
+        gpu_ctx.encode_bands(W, H, band_rows, r, world, buf.data_ptr(), rb.slot_elems, 1,
+                             gathered[r * stride:].data_ptr(), size.data_ptr(), s)
+        torch.cuda.synchronize()
+        total += int(size.item())
+    frame = torch.full((W * H,), -1, dtype=torch.int32, device="cuda")
+    gpu_ctx.decode_gathered(W, H, band_rows, world, gathered.data_ptr(), stride, 1, frame.data_ptr(), W * H, s)
+    torch.cuda.synchronize()
+    assert np.array_equal(frame.cpu().numpy().reshape(H, W), full)
+    assert total < 3 * W * H  # smaller than the RGB24 band sets
+
+
+def test_encode_rejects_bad_arguments(gpu_ctx):
+    import torch
+    from raytracer_hip import RayTracerError
+    buf = torch.zeros(64 * 64, dtype=torch.int32, device="cuda")
+    wire = torch.zeros(1 << 16, dtype=torch.uint8, device="cuda")
+    with pytest.raises(RayTracerError):  # rank out of range
+        gpu_ctx.encode_bands(64, 64, 8, 2, 2, buf.data_ptr(), 64 * 32, 1, wire.data_ptr())
+    with pytest.raises(RayTracerError):  # frame stride smaller than the band set
+        gpu_ctx.encode_bands(64, 64, 8, 0, 1, buf.data_ptr(), 64, 1, wire.data_ptr())
+    with pytest.raises(RayTracerError):  # misaligned wire
+        gpu_ctx.encode_bands(64, 64, 8, 0, 1, buf.data_ptr(), 64 * 64, 1, wire.data_ptr() + 4)

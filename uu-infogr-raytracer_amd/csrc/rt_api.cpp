@@ -82,6 +82,8 @@ struct Device {
     size_t bands_cap = 0;
     int32_t* d_gather = nullptr;  // device 0: n_gpus x padded band sets
     size_t gather_cap = 0;
+    void* d_stage = nullptr;  // rt_encode_bands scratch (encodes on one context are stream-ordered)
+    size_t stage_cap = 0;
     int32_t* d_frames2[2] = {nullptr, nullptr};  // rt_render_async double buffer
     size_t frames2_cap[2] = {0, 0};
     hipStream_t slot_stream[2] = {nullptr, nullptr};  // one per buffer: two frames in flight
@@ -493,6 +495,7 @@ void rt_destroy(rt_ctx* ctx) {
             if (d.d_frames2[i]) (void)hipFree(d.d_frames2[i]);
         if (d.d_counters) (void)hipFree(d.d_counters);
         if (d.d_view_tab) (void)hipFree(d.d_view_tab);
+        if (d.d_stage) (void)hipFree(d.d_stage);
         for (hipStream_t s : d.slot_stream)
             if (s) (void)hipStreamDestroy(s);
         if (d.stream) (void)hipStreamDestroy(d.stream);
@@ -743,6 +746,80 @@ int rt_scatter_gathered(rt_ctx* ctx, int width, int height, int band_rows, int w
     int e = launch_scatter_gathered((const unsigned char*)d_gathered, slot_bytes, format, d_frame, width, height,
                                     band_rows, world, hip_stream);
     if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "scatter launch: %s", hipGetErrorString((hipError_t)e));
+    return RT_OK;
+}
+
+// Tile-codec wire geometry (raytracer_hip/tilecodec.py.layout): the tile grid of the
+// largest band set, n_frames grids per batch, chunks of 64 tiles.
+static bool codec_geom(int width, int height, int band_rows, int world, int n_frames, rtk::CodecGeom& g,
+                       rt_wire_layout* lay) {
+    if (width <= 0 || height <= 0 || band_rows <= 0 || world <= 0 || n_frames <= 0) return false;
+    const int rows = std::max(1, bands_of(height, band_rows, 0, world)) * band_rows;
+    const long long tx = (width + 7) / 8, ty = (rows + 7) / 8;
+    const long long tpf = tx * ty, nt = tpf * (long long)n_frames;
+    if (nt > (1LL << 26)) return false;  // 32-bit word offsets (<= 48 words per tile)
+    const long long nc = (nt + 15) / 16;  // chunks of 16 tiles (one wave's)
+    g = rtk::CodecGeom{};
+    g.W = width, g.H = height, g.band_rows = band_rows, g.world = world;
+    g.tiles_x = (int)tx, g.tiles_y = (int)ty, g.tiles_per_frame = (int)tpf, g.n_tiles = (int)nt, g.n_chunks = (int)nc;
+    g.fixed_bytes = ((size_t)16 + 8 * (size_t)nt + 4 * (size_t)nc + 7) / 8 * 8;
+    if (lay) {
+        lay->fixed_bytes = g.fixed_bytes;
+        lay->max_bytes = g.fixed_bytes + 8 * 24 * (size_t)nt;
+        lay->tiles_x = (int32_t)tx, lay->tiles_y = (int32_t)ty, lay->tiles_per_frame = (int32_t)tpf;
+        lay->n_frames = n_frames, lay->n_tiles = (int32_t)nt, lay->n_chunks = (int32_t)nc;
+    }
+    return true;
+}
+
+int rt_wire_layout_of(int width, int height, int band_rows, int world, int n_frames, rt_wire_layout* out) {
+    rtk::CodecGeom g;
+    if (!out || !codec_geom(width, height, band_rows, world, n_frames, g, out))
+        return fail(nullptr, RT_ERR_INVALID_ARG, "rt_wire_layout_of: bad arguments");
+    return RT_OK;
+}
+
+int rt_encode_bands(rt_ctx* ctx, int width, int height, int band_rows, int rank, int world, const int32_t* d_bands,
+                    size_t frame_stride, int n_frames, void* d_wire, int64_t* d_wire_bytes, void* hip_stream) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "NULL context");
+    rtk::CodecGeom g;
+    if (!codec_geom(width, height, band_rows, world, n_frames, g, nullptr) || rank < 0 || rank >= world ||
+        !d_bands || !d_wire || ((uintptr_t)d_wire & 7) != 0 ||
+        frame_stride < (size_t)std::max(1, bands_of(height, band_rows, 0, world)) * band_rows * width)
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_encode_bands: bad arguments");
+    g.rank = rank;
+    g.n_bands = bands_of(height, band_rows, rank, world);
+    g.frame_stride = frame_stride;
+    Device& d = ctx->dev[0];
+    DeviceGuard guard(d.id);
+    // codec scratch (staged segments + workgroup sums), grown on demand: the previous user of the
+    // old buffer may still run, so growing waits for the device first
+    const size_t need = encode_stage_bytes(g);
+    if (need > d.stage_cap) {
+        HIP_TRY(ctx, hipDeviceSynchronize());
+        if (d.d_stage) HIP_TRY(ctx, hipFree(d.d_stage));
+        d.d_stage = nullptr, d.stage_cap = 0;
+        HIP_TRY(ctx, hipMalloc(&d.d_stage, need));
+        d.stage_cap = need;
+    }
+    int e = launch_encode_bands(d_bands, (unsigned char*)d_wire, g, d_wire_bytes, d.d_stage, hip_stream);
+    if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "encode launch: %s", hipGetErrorString((hipError_t)e));
+    return RT_OK;
+}
+
+int rt_decode_gathered(rt_ctx* ctx, int width, int height, int band_rows, int world, const void* d_gathered,
+                       size_t rank_stride, int n_frames, int32_t* d_frames, size_t frame_stride, void* hip_stream) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "NULL context");
+    rtk::CodecGeom g;
+    if (!codec_geom(width, height, band_rows, world, n_frames, g, nullptr) || !d_gathered || !d_frames ||
+        ((uintptr_t)d_gathered & 7) != 0 || (rank_stride & 7) != 0 || (world > 1 && rank_stride < g.fixed_bytes) ||
+        frame_stride < (size_t)width * height)
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_decode_gathered: bad arguments");
+    g.frame_stride = frame_stride;
+    Device& d = ctx->dev[0];
+    DeviceGuard guard(d.id);
+    int e = launch_decode_gathered((const unsigned char*)d_gathered, rank_stride, d_frames, g, hip_stream);
+    if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "decode launch: %s", hipGetErrorString((hipError_t)e));
     return RT_OK;
 }
 

@@ -139,4 +139,21 @@ int launch_scatter_gathered(const unsigned char* g, size_t slot_bytes, int fmt, 
 int launch_scatter_bands(const int32_t* bands, int32_t* frame, int W, int H, int band_rows, int band_first,
                          int band_step, int n_bands, void* stream);
 
+// Band-set tile codec (rt_codec.hip; format: raytracer_hip/tilecodec.py).
+struct CodecGeom {
+    int W, H, band_rows, rank, world, n_bands;  // n_bands: bands of `rank` (encoder)
+    int tiles_x, tiles_y, tiles_per_frame, n_tiles, n_chunks;
+    size_t frame_stride;  // elements between frames (input band sets / output frames)
+    size_t fixed_bytes;   // wire: header + tile headers + chunk bases, 8-aligned
+};
+// n_frames band sets (frame_stride apart) of g.rank -> wire; *wire_bytes (device, may be
+// NULL) receives the wire's byte size.  Two launches; `stage` = encode_stage_bytes(g) of
+// device scratch that no other launch uses meanwhile.
+int launch_encode_bands(const int32_t* bands, unsigned char* wire, const CodecGeom& g, int64_t* wire_bytes,
+                        void* stage, void* stream);
+size_t encode_stage_bytes(const CodecGeom& g);
+// every rank's wire (rank r's at gathered + r * rank_stride) -> frames.  One launch.
+int launch_decode_gathered(const unsigned char* gathered, size_t rank_stride, int32_t* frames, const CodecGeom& g,
+                           void* stream);
+
 }  // namespace rtk

@@ -22,7 +22,7 @@ from .debugview import SEGMENT_DTYPE, DebugView, surface_line
 from .dist import bands_of
 
 __all__ = ["Surface", "RayTracer", "Context", "RayTracerError", "scenes", "abi", "load_library",
-           "device_count", "camera_view", "bands_of", "DebugView", "SEGMENT_DTYPE", "debugview"]
+           "device_count", "camera_view", "wire_layout", "bands_of", "DebugView", "SEGMENT_DTYPE", "debugview"]
 
 
 def device_count() -> int:
@@ -30,6 +30,14 @@ def device_count() -> int:
     n = C.c_int(0)
     check(lib, lib.rt_device_count(C.byref(n)))
     return n.value
+
+
+def wire_layout(width: int, height: int, band_rows: int, world: int, n_frames: int = 1) -> abi.rt_wire_layout:
+    """rt_wire_layout_of: sizes of one rank's tile-codec wire (host only, no device needed)."""
+    lib = load_library()
+    out = abi.rt_wire_layout()
+    check(lib, lib.rt_wire_layout_of(width, height, band_rows, world, n_frames, C.byref(out)))
+    return out
 
 
 def camera_view(camera: abi.rt_camera, width: int, height: int) -> abi.rt_view:
@@ -145,6 +153,20 @@ class Context:
         """Reassemble all ranks' band sets (rank r's at d_gathered + r * rank_stride) into d_frame."""
         self._check(self.lib.rt_scatter_gathered(self.ptr, width, height, band_rows, world, C.c_void_p(d_gathered),
                                                  rank_stride, fmt, C.c_void_p(d_frame), C.c_void_p(stream)))
+
+    def encode_bands(self, width: int, height: int, band_rows: int, rank: int, world: int, d_bands: int,
+                     frame_stride: int, n_frames: int, d_wire: int, d_wire_bytes: int = 0, stream: int = 0):
+        """Tile-encode n_frames band sets of `rank` into the wire at d_wire (rt_encode_bands)."""
+        self._check(self.lib.rt_encode_bands(self.ptr, width, height, band_rows, rank, world, C.c_void_p(d_bands),
+                                             frame_stride, n_frames, C.c_void_p(d_wire),
+                                             C.c_void_p(d_wire_bytes or None), C.c_void_p(stream)))
+
+    def decode_gathered(self, width: int, height: int, band_rows: int, world: int, d_gathered: int,
+                        rank_stride: int, n_frames: int, d_frames: int, frame_stride: int, stream: int = 0):
+        """Decode every rank's wire (rank r's at d_gathered + r * rank_stride) into the frames."""
+        self._check(self.lib.rt_decode_gathered(self.ptr, width, height, band_rows, world, C.c_void_p(d_gathered),
+                                                rank_stride, n_frames, C.c_void_p(d_frames), frame_stride,
+                                                C.c_void_p(stream)))
 
     def render_async(self, width: int, height: int, out: np.ndarray):
         """Double-buffered Tick (rt_render_async): returns at once; `wait()` before reading `out`."""

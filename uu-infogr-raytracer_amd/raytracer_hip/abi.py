@@ -13,7 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
 LIB_PATH = os.path.join(PKG_ROOT, "lib", "libraytracer_hip.so")
 
-RT_ABI_VERSION = 3  # include/raytracer_hip.h
+RT_ABI_VERSION = 4  # include/raytracer_hip.h
 RT_BANDS_INT32, RT_BANDS_RGB24 = 0, 1
 RT_OK = 0
 RT_ERR_INVALID_ARG = -1
@@ -80,6 +80,13 @@ class rt_stats(C.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class rt_wire_layout(C.Structure):
+    _fields_ = [
+        ("fixed_bytes", C.c_uint64), ("max_bytes", C.c_uint64), ("tiles_x", C.c_int32), ("tiles_y", C.c_int32),
+        ("tiles_per_frame", C.c_int32), ("n_frames", C.c_int32), ("n_tiles", C.c_int32), ("n_chunks", C.c_int32),
+    ]
+
+
 # (name, restype, argtypes) of every exported entry point declared in the header.
 EXPORTS = [
     ("rt_abi_version", C.c_int, []),
@@ -106,6 +113,11 @@ EXPORTS = [
                                      C.c_void_p, C.POINTER(C.c_int)]),
     ("rt_scatter_gathered", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_size_t,
                                       C.c_int, C.c_void_p, C.c_void_p]),
+    ("rt_wire_layout_of", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(rt_wire_layout)]),
+    ("rt_encode_bands", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_size_t,
+                                  C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("rt_decode_gathered", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_size_t,
+                                     C.c_int, C.c_void_p, C.c_size_t, C.c_void_p]),
     ("rt_render_async", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     ("rt_wait", C.c_int, [C.c_void_p]),
     ("rt_write_ppm", C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),

@@ -226,3 +226,160 @@ class BatchedBandGather:
             out.append((self.gathered[pi], pn))
             self.pending = None
         return out
+
+
+class TileBandGather:
+    """Tile-encoded band sets, F frames per batch, three-stage pipeline (bench.py's N > 1 step).
+
+    Rendered frames are mostly flat, so shipping them to rank 0 raw (3-4 bytes per pixel)
+    spends xGMI bandwidth on redundancy; each rank tile-encodes its batch (rt_encode_bands,
+    format in raytracer_hip/tilecodec.py) and rank 0 decodes every rank's wire straight into
+    its frames (rt_decode_gathered).  A wire's size varies with the image, and a gather moves
+    the same count from every rank, so each batch costs two collectives:
+
+        A  encode batch b into wire b % 3; all_reduce(MAX) of the wire sizes   (async)
+        B  batch b-1: wait for its all_reduce, read the max size on the host, gather that
+           many bytes of every rank's wire into rank 0's receive buffer (b-1) % 2  (async)
+        C  batch b-2 (rank 0): wait for its gather, decode all ranks' wires into the frames
+
+    run at every batch boundary, so the host waits only for a size that was reduced one batch
+    earlier while the GPU traces the current batch.  On GPUs the waits for collectives are put
+    on two side streams (`comm`, `dec`), never on the trace streams; events order buffer reuse
+    (wire b % 3 is re-encoded only after gather b completed, receive buffer b % 2 is
+    overwritten only after decode b).  With gloo on CPU tensors (tests) the same sequence runs
+    synchronously.
+
+        raw = g.raw_frame(k)       -> int32 tensor view: this rank's band set of frame k
+        g.commit(main_stream)      -> after frame k was traced (run stages at batch ends)
+        g.drain()                  -> submit a partial last batch and finish every stage
+    `encode(raw_batch, n_frames, wire, size_tensor, stream)` and
+    `decode(gathered, rank_stride, n_frames, frames, stream)` do the codec work (the HIP library
+    on GPUs, the host mirror in tests); `frames` (rank 0) holds F decoded frames.
+    """
+
+    def __init__(self, rb: RowBands, device, frames_per_batch, layout_fn, encode, decode):
+        import torch
+        self.rb, self.F, self.device = rb, max(1, frames_per_batch), torch.device(device)
+        self.cuda = self.device.type == "cuda"
+        self.layout_fn, self.encode, self.decode = layout_fn, encode, decode
+        self.slot_elems = rb.slot_elems
+        lay = layout_fn(self.F)
+        self.rank_stride = (int(lay.max_bytes) + 255) // 256 * 256
+        self.raw = [torch.zeros(self.F * self.slot_elems, dtype=torch.int32, device=self.device) for _ in range(2)]
+        self.wire = [torch.zeros(self.rank_stride, dtype=torch.uint8, device=self.device) for _ in range(3)]
+        self.size = [torch.zeros(1, dtype=torch.int64, device=self.device) for _ in range(3)]
+        self.size_host = torch.zeros(3, dtype=torch.int64, pin_memory=self.cuda)
+        self.recv = ([torch.zeros(rb.world * self.rank_stride, dtype=torch.uint8, device=self.device)
+                      for _ in range(2)] if rb.rank == 0 else [None, None])
+        self.frames = (torch.zeros(self.F * rb.width * rb.height, dtype=torch.int32, device=self.device)
+                       if rb.rank == 0 else None)
+        if self.cuda:
+            self.comm, self.dec = torch.cuda.Stream(self.device), torch.cuda.Stream(self.device)
+        self.k = 0             # frames rendered
+        self.batch = 0         # batches encoded
+        self.stage_b = []      # [(batch, n_frames, all_reduce work)]
+        self.stage_c = []      # [(batch, n_frames, gather work)]
+        self.gathered_ev = {}  # batch -> event after its gather (wire reusable)
+        self.decoded_ev = {}   # batch -> event after its decode (receive buffer reusable)
+        self.decoded = 0       # batches decoded (rank 0)
+        self.bytes_sent = 0    # wire bytes gathered per rank (sum over batches)
+
+    def raw_frame(self, k=None):
+        k = self.k if k is None else k
+        i = (k // self.F) % 2
+        o = (k % self.F) * self.slot_elems
+        return self.raw[i][o:o + self.slot_elems]
+
+    # -- stages -------------------------------------------------------------------
+    def _stage_a(self, main, n_frames):
+        import torch.distributed as dist
+        b = self.batch
+        i = b % 3
+        while self.stage_b and self.stage_b[0][0] <= b - 3:  # (no-ops in steady state)
+            self._stage_b()
+        while self.stage_c and self.stage_c[0][0] <= b - 3:
+            self._stage_c()
+        if b - 3 in self.gathered_ev:  # wire i was last read by gather b-3
+            ev = self.gathered_ev.pop(b - 3)
+            if self.cuda:
+                main.wait_event(ev)
+        self.encode(self.raw[b % 2], n_frames, self.wire[i], self.size[i], main)
+        work = dist.all_reduce(self.size[i], op=dist.ReduceOp.MAX, async_op=True)
+        self.stage_b.append((b, n_frames, work))
+        self.batch += 1
+
+    def _stage_b(self):
+        import torch
+        import torch.distributed as dist
+        b = self.stage_b[0][0]
+        while self.stage_c and self.stage_c[0][0] <= b - 2:  # receive buffer b % 2 is free again
+            self._stage_c()
+        b, n_frames, work = self.stage_b.pop(0)
+        i = b % 3
+        if self.cuda:
+            with torch.cuda.stream(self.comm):
+                work.wait()
+                self.size_host[i:i + 1].copy_(self.size[i], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.comm)
+            ev.synchronize()
+        else:
+            work.wait()
+            self.size_host[i] = self.size[i][0]
+        n = int(self.size_host[i])
+        n = (n + 7) // 8 * 8
+        self.bytes_sent += n
+        j = b % 2
+        glist = None
+        if self.rb.rank == 0:
+            glist = [self.recv[j][r * self.rank_stride:r * self.rank_stride + n] for r in range(self.rb.world)]
+        if self.cuda:
+            with torch.cuda.stream(self.comm):
+                if b - 2 in self.decoded_ev:  # receive buffer j was last read by decode b-2
+                    self.comm.wait_event(self.decoded_ev.pop(b - 2))
+                gw = dist.gather(self.wire[i][:n], glist, dst=0, async_op=True)
+        else:
+            gw = dist.gather(self.wire[i][:n], glist, dst=0, async_op=True)
+        self.stage_c.append((b, n_frames, gw))
+
+    def _stage_c(self):
+        import torch
+        b, n_frames, gw = self.stage_c.pop(0)
+        if self.cuda:
+            with torch.cuda.stream(self.dec):
+                gw.wait()
+                ev = torch.cuda.Event()
+                ev.record(self.dec)
+                self.gathered_ev[b] = ev
+                if self.rb.rank == 0:
+                    self.decode(self.recv[b % 2], self.rank_stride, n_frames, self.frames, self.dec)
+                    dv = torch.cuda.Event()
+                    dv.record(self.dec)
+                    self.decoded_ev[b] = dv
+        else:
+            gw.wait()
+            self.gathered_ev[b] = None
+            if self.rb.rank == 0:
+                self.decode(self.recv[b % 2], self.rank_stride, n_frames, self.frames, None)
+                self.decoded_ev[b] = None
+        if self.rb.rank == 0:
+            self.decoded += 1
+
+    def commit(self, main=None):
+        """Frame k traced (on `main`'s stream or joined into it).  At a batch end: stages A, B, C."""
+        self.k += 1
+        if self.k % self.F == 0:
+            self._stage_a(main, self.F)
+            if len(self.stage_b) > 1:
+                self._stage_b()
+            if len(self.stage_c) > 1:
+                self._stage_c()
+
+    def drain(self, main=None):
+        if self.k % self.F:
+            self._stage_a(main, self.k % self.F)
+            self.k += self.F - self.k % self.F
+        while self.stage_b:
+            self._stage_b()
+        while self.stage_c:
+            self._stage_c()
