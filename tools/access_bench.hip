@@ -33,6 +33,20 @@ __global__ void tiles(const int* __restrict__ a, int W, int tiles_x, int n_tiles
     if (acc == 0x12345678u) out[0] = acc;
 }
 
+// decoder store pattern: lane 8j+ry writes row ry (8 pixels, 2 x 16 B) of tile g*8+j
+__global__ void store_rows(int* __restrict__ a, int W, int tiles_x, int n_tiles, int stride_loop) {
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int groups = n_tiles / 8;
+    for (int g = blockIdx.x * 4 + wave; g < groups; g += stride_loop ? gridDim.x * 4 : groups) {
+        const int t = g * 8 + (lane >> 3), ry = lane & 7;
+        const int tr = t / tiles_x, tc = t - tr * tiles_x;
+        int4* d = (int4*)(a + (size_t)(tr * 8 + ry) * W + tc * 8);
+        d[0] = make_int4(t, t, t, t);
+        d[1] = make_int4(t, t, t, t);
+    }
+}
+
 int main() {
     const int W = 1920, H = 1080 * 8;
     const size_t n = (size_t)W * H;
@@ -61,5 +75,7 @@ int main() {
     run("tiles16 grid 2048", [&] { hipLaunchKernelGGL(tiles<16>, dim3(2048), dim3(256), 0, 0, a, W, tx, nt, out); });
     run("tiles4 full grid", [&] { hipLaunchKernelGGL(tiles<4>, dim3((nt / 4 + 3) / 4), dim3(256), 0, 0, a, W, tx, nt, out); });
     run("tiles1 full grid", [&] { hipLaunchKernelGGL(tiles<1>, dim3((nt + 3) / 4), dim3(256), 0, 0, a, W, tx, nt, out); });
+    run("store_rows full grid", [&] { hipLaunchKernelGGL(store_rows, dim3((nt / 8 + 3) / 4), dim3(256), 0, 0, a, W, tx, nt, 0); });
+    run("store_rows grid 2048", [&] { hipLaunchKernelGGL(store_rows, dim3(2048), dim3(256), 0, 0, a, W, tx, nt, 1); });
     return 0;
 }

@@ -1,0 +1,1 @@
+cd ${GRAFT_REPO_ROOT}; timeout -k 10 60 ./tools/access_bench

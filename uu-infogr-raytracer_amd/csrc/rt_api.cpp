@@ -758,7 +758,7 @@ static bool codec_geom(int width, int height, int band_rows, int world, int n_fr
     const long long tx = (width + 7) / 8, ty = (rows + 7) / 8;
     const long long tpf = tx * ty, nt = tpf * (long long)n_frames;
     if (nt > (1LL << 26)) return false;  // 32-bit word offsets (<= 48 words per tile)
-    const long long nc = (nt + 15) / 16;  // chunks of 16 tiles (one wave's)
+    const long long nc = (nt + 7) / 8;  // chunks of 8 tiles (one wave's)
     g = rtk::CodecGeom{};
     g.W = width, g.H = height, g.band_rows = band_rows, g.world = world;
     g.tiles_x = (int)tx, g.tiles_y = (int)ty, g.tiles_per_frame = (int)tpf, g.n_tiles = (int)nt, g.n_chunks = (int)nc;

@@ -8,14 +8,14 @@
 // predicted by its left neighbour, the first column by the pixel above (odd rows) or by the
 // tile's first pixel (even rows) -- predictors a DPP row shift or a scalar can deliver; per
 // channel residuals mod 256, zigzag; widths rounded up to 0/1/2/4/8 bits, lane-packed.
-// Tiles are grouped in chunks of 64; a tile's payload lives at its chunk's base + its offset
+// Tiles are grouped in chunks of 8; a tile's payload lives at its chunk's base + its offset
 // inside the chunk.
 //
-// Encode = two launches per batch of frames (deterministic layout, no atomics), chunks of 16
+// Encode = two launches per batch of frames (deterministic layout, no atomics), chunks of 8
 // tiles = one wave's, contiguous ranges of chunks per workgroup:
 //   encode_tiles_kernel  residuals, widths, packed segments (into the context's staging slot
-//                        of 48 words per tile), chunk-relative offsets -> tile headers; chunk
-//                        totals -> chunk_base[] (in place), range totals -> wg_total[]
+//                        of 48 words per tile, final byte layout), chunk-relative offsets ->
+//                        tile headers; chunk totals -> chunk_base[], range totals -> wg_total[]
 //   encode_copy_kernel   range base = sum of the earlier ranges' totals, chunk bases by an LDS
 //                        scan, staged segments -> compact offsets; wire header and size
 // Decode = one launch for every rank's wire of a batch (decode_tiles_kernel).
@@ -31,10 +31,11 @@
 
 namespace rtk {
 
-constexpr int CODEC_TPW = 16;    // tiles per wave = tiles per chunk
+constexpr int CODEC_TPW = 8;     // tiles per wave = tiles per chunk
 constexpr int CODEC_BLOCKS = 2048;   // resident grid: 256 CUs x 8 workgroups of 4 waves
 constexpr int CODEC_MAX_PER = 1024;  // chunks per workgroup at most (LDS of the copy pass)
 constexpr int STAGE_WORDS = 48;  // staging words per tile (3 channels x 8 bits x 64 lanes / 32)
+constexpr int STAGE_UNITS = STAGE_WORDS / 2;
 
 // Wave index inside the workgroup, as a scalar: what derives from it stays wave-uniform.
 __device__ __forceinline__ int wave_index() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
@@ -85,176 +86,111 @@ __device__ __forceinline__ int frame_row(const CodecGeom& g, int rank, int r) {
     return (rank + (r / g.band_rows) * g.world) * g.band_rows + r % g.band_rows;
 }
 
-// Per-tile bookkeeping is lane-parallel: lane j (< CODEC_TPW) of a wave describes tile t0 + j
-// of its chunk (frame, tile row / column, where its pixels live, which are inside the frame),
-// and the tile loop fetches what it needs with readlane -- so the scalar unit, which all waves
-// of a CU share, stays nearly idle.  When band_rows % 8 == 0 (the shipped 8) a tile lies
-// inside one band: its frame rows are y0 + ry and a pixel is inside iff rx < x_lim and
-// ry < y_lim; otherwise every pixel maps its own row (generic path).
-struct TileInfo {
-    int tr;        // tile row (generic path)
-    int x_lim;     // columns inside the frame: rx < x_lim
-    int y_lim;     // rows inside (band_rows % 8 == 0): ry < y_lim
-    int64_t src;   // element offset of the tile's pixel (0, 0) in the band sets
-    int64_t dst;   // element offset of the tile's pixel (0, 0) in the frames (band_rows % 8 == 0)
-    bool live;     // t0 + j < n_tiles
+// Both directions use one layout: lane L = 8 j + ry of a wave handles row ry (8 pixels) of
+// tile t0 + j of a group of CODEC_TPW = 8 consecutive tiles (= one chunk).  A row's residuals
+// of one channel are then the w consecutive bytes [ry*w, ry*w + w) of the channel's segment,
+// the left-neighbour prediction / prefix runs in registers, the first column needs only the
+// lane above (DPP row shift by one) and the tile's first pixel (one bpermute), and a tile's
+// OR of residuals is a 3-step DPP OR inside its 8 lanes.
+
+// Tile position of this lane's tile (t0 + j): t0's by scalar divisions, then stepping
+// (tiles_x >= 8 wraps at most once; narrow frames loop).
+struct TilePos {
+    int f, tr, tc;
 };
-__device__ __forceinline__ TileInfo tile_info(const CodecGeom& g, int rank, int nb, int t) {
-    TileInfo ti;
-    ti.live = t < g.n_tiles;
-    const int tc0 = ti.live ? t : 0;
-    const int f = tc0 / g.tiles_per_frame;
-    const int tt = tc0 - f * g.tiles_per_frame;
-    ti.tr = tt / g.tiles_x;
-    const int tc = tt - ti.tr * g.tiles_x;
-    const int r0 = ti.tr * 8;
-    ti.x_lim = g.W - tc * 8;
-    ti.src = (int64_t)f * (int64_t)g.frame_stride + (int64_t)r0 * g.W + tc * 8;
-    ti.y_lim = 0, ti.dst = 0;
-    if ((g.band_rows & 7) == 0) {
-        const int k = r0 / g.band_rows;
-        const int y0 = (rank + k * g.world) * g.band_rows + (r0 - k * g.band_rows);
-        ti.y_lim = min(nb * g.band_rows - r0, g.H - y0);
-        ti.dst = (int64_t)f * (int64_t)g.frame_stride + (int64_t)y0 * g.W + tc * 8;
-    } else {
-        ti.dst = (int64_t)f * (int64_t)g.frame_stride + tc * 8;  // + y * W per pixel
+__device__ __forceinline__ TilePos tile_pos(const CodecGeom& g, int t0, int j) {
+    const int f0 = t0 / g.tiles_per_frame;
+    const int tt0 = t0 - f0 * g.tiles_per_frame;
+    const int tr0 = tt0 / g.tiles_x;
+    TilePos p{f0, tr0, tt0 - tr0 * g.tiles_x + j};
+    while (p.tc >= g.tiles_x) {
+        p.tc -= g.tiles_x;
+        if (++p.tr == g.tiles_y) p.tr = 0, ++p.f;
     }
-    if (!ti.live) ti.x_lim = 0, ti.y_lim = 0;
-    return ti;
-}
-__device__ __forceinline__ int64_t readlane64(int64_t v, int j) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, j);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)v >> 32), j);
-    return (int64_t)(((uint64_t)hi << 32) | lo);
-}
-// This lane's pixel of tile j (lane-parallel info `ti`): inside the frame?  *y_off = the
-// element offset of its frame row relative to the tile's dst (generic path: absolute row).
-__device__ __forceinline__ bool pixel_inside(const CodecGeom& g, int rank, int nb, const TileInfo& ti, int j, int lane,
-                                             int64_t* row_off) {
-    const int rx = lane & 7, ry = lane >> 3;
-    const int x_lim = __builtin_amdgcn_readlane(ti.x_lim, j);
-    if ((g.band_rows & 7) == 0) {
-        const int y_lim = __builtin_amdgcn_readlane(ti.y_lim, j);
-        *row_off = (int64_t)ry * g.W;
-        return rx < x_lim && ry < y_lim;
-    }
-    const int r = __builtin_amdgcn_readlane(ti.tr, j) * 8 + ry;
-    const int y = frame_row(g, rank, r);
-    *row_off = (int64_t)y * g.W;
-    return rx < x_lim && r < nb * g.band_rows && y < g.H;
+    return p;
 }
 
-// Zigzag residuals (packed 0x00RRGGBB) of this lane's pixel v (0 outside the frame; a valid
-// pixel's predictor is valid too); converged wave call.
-__device__ __forceinline__ uint32_t tile_residual(uint32_t v, bool valid, int lane, uint32_t first) {
-    const uint32_t left = row_shr<1>(v), above = row_shr<8>(v);
-    const uint32_t pred = (lane & 7) ? left : ((lane & 8) ? above : first);
-    return valid ? zigzag_bytes(sub_bytes(v, pred)) & 0xffffffu : 0u;
-}
-
-// OR of z over the wave (DPP OR-scan inside each 16-lane row, then the four row totals).
-__device__ __forceinline__ uint32_t wave_or(uint32_t z) {
-    z |= row_shr<1>(z);
-    z |= row_shr<2>(z);
-    z |= row_shr<4>(z);
-    z |= row_shr<8>(z);
-    return (uint32_t)__builtin_amdgcn_readlane((int)z, 15) | (uint32_t)__builtin_amdgcn_readlane((int)z, 31) |
-           (uint32_t)__builtin_amdgcn_readlane((int)z, 47) | (uint32_t)__builtin_amdgcn_readlane((int)z, 63);
-}
 // Width of a channel: bit length of its OR rounded up to 0, 1, 2, 4 or 8.
 __device__ __forceinline__ uint32_t width_of(uint32_t o) {
     return o == 0 ? 0u : o < 2 ? 1u : o < 4 ? 2u : o < 16 ? 4u : 8u;
 }
 
-// DPP quad permutations (inside each group of 4 lanes).
-__device__ __forceinline__ uint32_t quad_swap1(uint32_t v) {  // [1,0,3,2]
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xb1, 0xf, 0xf, false);
-}
-__device__ __forceinline__ uint32_t quad_swap2(uint32_t v) {  // [2,3,0,1]
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4e, 0xf, 0xf, false);
-}
-
-// Pack channel values x (0..2^w-1, this lane's) of width w into 2w words at seg: lane l's
-// bits at l*w of the stream.  A word gathers 32/w lanes (a DPP OR inside the group), the
-// group's last lane stores it.  Converged wave call, w in {1, 2, 4, 8} (wave-uniform).
-__device__ __forceinline__ void pack_segment(uint32_t* __restrict__ seg, uint32_t x, uint32_t w, int lane) {
-    if (w == 1) {
-        const uint64_t m = __builtin_amdgcn_ballot_w64(x != 0);
-        if (lane < 2) seg[lane] = lane == 0 ? (uint32_t)m : (uint32_t)(m >> 32);
-        return;
-    }
-    uint32_t y = x << ((lane * w) & 31);
-    y |= quad_swap1(y);
-    y |= quad_swap2(y);  // every lane: its quad's OR (w = 8: one word per quad)
-    if (w <= 4) y |= row_shr<4>(y);  // lanes 8k+7: the OR of their 8 lanes (w = 4: one word)
-    if (w == 2) y |= row_shr<8>(y);  // lanes 16k+15: the OR of their 16 lanes
-    const int group = 32 / (int)w;
-    if ((lane & (group - 1)) == group - 1) seg[lane / group] = y;
-}
-
-// One wave per chunk of CODEC_TPW consecutive tiles, their loads issued together
-// (unconditional loads from a safe address for pixels outside the frame: no branch, no wait).
-// Writes the tile headers with chunk-relative offsets, the chunk total into chunk_base[]
-// (scanned next) and the non-flat tiles' segments into their staging slots.
-__device__ __forceinline__ uint32_t encode_chunk(const int32_t* __restrict__ bands, unsigned char* __restrict__ wire,
+// Encode one group of CODEC_TPW tiles (one chunk): tile headers with chunk-relative offsets,
+// the chunk total into chunk_base[chunk], the non-flat tiles' segments into their staging
+// slots (STAGE_WORDS per tile, final byte layout).  Returns the chunk total (units).
+__device__ __forceinline__ uint32_t encode_group(const int32_t* __restrict__ bands, unsigned char* __restrict__ wire,
                                                  uint32_t* __restrict__ stage, const CodecGeom& g, int chunk, int lane) {
     const int t0 = chunk * CODEC_TPW;
-    const TileInfo ti = tile_info(g, g.rank, g.n_bands, t0 + (lane & (CODEC_TPW - 1)));
-    uint32_t v[CODEC_TPW];
-    bool ok[CODEC_TPW];
-    const int64_t lane_off = (int64_t)(lane >> 3) * g.W + (lane & 7);
+    const int j = lane >> 3, ry = lane & 7;
+    const int t = t0 + j;
+    const bool live = t < g.n_tiles;
+    const TilePos tp = tile_pos(g, t0, j);
+    const int r = tp.tr * 8 + ry;
+    const bool row_ok = live && r < g.n_bands * g.band_rows && frame_row(g, g.rank, r) < g.H;
+    const int x0 = tp.tc * 8;
+    const int ncols = row_ok ? min(8, g.W - x0) : 0;
+    const int32_t* src = bands + (size_t)tp.f * g.frame_stride + (size_t)r * (size_t)g.W + (size_t)x0;
+    uint32_t p[8];
+    if (ncols == 8 && ((uintptr_t)src & 15) == 0) {
+        const int4 a = ((const int4*)src)[0], b = ((const int4*)src)[1];
+        p[0] = (uint32_t)a.x, p[1] = (uint32_t)a.y, p[2] = (uint32_t)a.z, p[3] = (uint32_t)a.w;
+        p[4] = (uint32_t)b.x, p[5] = (uint32_t)b.y, p[6] = (uint32_t)b.z, p[7] = (uint32_t)b.w;
+    } else {
 #pragma unroll
-    for (int j = 0; j < CODEC_TPW; ++j) {
-        int64_t row_off;
-        ok[j] = pixel_inside(g, g.rank, g.n_bands, ti, j, lane, &row_off);
-        const int64_t off = readlane64(ti.src, j) + lane_off;
-        const uint32_t raw = (uint32_t)bands[ok[j] ? off : 0];
-        v[j] = ok[j] ? raw & 0xffffffu : 0u;
+        for (int rx = 0; rx < 8; ++rx) p[rx] = rx < ncols ? (uint32_t)src[rx] : 0u;
     }
-    uint32_t z[CODEC_TPW];
-    uint32_t lane_first = 0, lane_or = 0;  // lane j: tile j's first pixel / OR of residuals
 #pragma unroll
-    for (int j = 0; j < CODEC_TPW; ++j) {
-        const uint32_t first = (uint32_t)__builtin_amdgcn_readfirstlane((int)v[j]);  // lane 0 (0 if outside)
-        z[j] = tile_residual(v[j], ok[j], lane, first);
-        const uint32_t o = wave_or(z[j]);
-        if (lane == j) lane_first = first, lane_or = o;
-    }
-    // lane-parallel over the chunk's tiles: widths, units, chunk-relative offsets
-    const uint32_t wm = width_of((lane_or >> 16) & 0xffu) | (width_of((lane_or >> 8) & 0xffu) << 4) |
-                        (width_of(lane_or & 0xffu) << 8);
-    const uint32_t u = lane < CODEC_TPW ? units_of(wm) : 0u;
-    uint32_t incl = u;  // inclusive prefix over lanes 0..15 (DPP row 0)
-    uint32_t o = row_shr<1>(incl);
-    incl += o;
-    o = row_shr<2>(incl);
-    incl += o;
-    o = row_shr<4>(incl);
-    incl += o;
-    o = row_shr<8>(incl);
-    incl += o;
-    const uint32_t meta = wm | ((incl - u) << 12);
-    if (lane < CODEC_TPW && ti.live) {
-        uint32_t* h = wire_tile_hdr(wire) + 2 * (size_t)(t0 + lane);
-        h[0] = lane_first;
-        h[1] = meta;
-    }
-    if (lane == CODEC_TPW - 1) wire_chunk_base(wire, g)[chunk] = incl;  // chunk total
-    // segments of the non-flat tiles -> staging slot (48 words per tile)
+    for (int rx = 0; rx < 8; ++rx) p[rx] &= 0xffffffu;  // pixels outside the frame are 0
+    // residuals: left neighbour; first column: above (odd rows) or the tile's first pixel
+    const uint32_t first = (uint32_t)__shfl((int)p[0], lane & ~7, 64);
+    const uint32_t above = row_shr<1>(p[0]);
+    uint32_t z[8];
+    z[0] = ncols > 0 ? zigzag_bytes(sub_bytes(p[0], (ry & 1) ? above : first)) & 0xffffffu : 0u;
 #pragma unroll
-    for (int j = 0; j < CODEC_TPW; ++j) {
-        const uint32_t mj = (uint32_t)__builtin_amdgcn_readlane((int)meta, j);
-        if ((mj & 0xfffu) == 0) continue;  // flat tile (wave-uniform)
-        uint32_t* seg = stage + (size_t)(t0 + j) * STAGE_WORDS;
+    for (int rx = 1; rx < 8; ++rx) z[rx] = rx < ncols ? zigzag_bytes(sub_bytes(p[rx], p[rx - 1])) & 0xffffffu : 0u;
+    // tile OR of residuals -> widths (lane 8j+7 accumulates lanes 8j..8j+7), broadcast
+    uint32_t o = z[0] | z[1] | z[2] | z[3] | z[4] | z[5] | z[6] | z[7];
+    o |= row_shr<1>(o);
+    o |= row_shr<2>(o);
+    o |= row_shr<4>(o);
+    uint32_t wm = width_of((o >> 16) & 0xffu) | (width_of((o >> 8) & 0xffu) << 4) | (width_of(o & 0xffu) << 8);
+    wm = (uint32_t)__shfl((int)wm, lane | 7, 64);
+    if (!live) wm = 0;
+    const uint32_t u = units_of(wm);
+    // chunk-relative offsets: inclusive scan over the group leaders (lanes 8j+7)
+    uint32_t incl = ry == 7 ? u : 0u;
+#pragma unroll
+    for (int k = 8; k < 64; k <<= 1) {
+        const uint32_t x = (uint32_t)__shfl_up((int)incl, k, 64);
+        if (lane >= k) incl += x;
+    }
+    const uint32_t rel = (uint32_t)__shfl((int)(incl - u), lane | 7, 64);
+    if (live && ry == 0) ((uint2*)wire_tile_hdr(wire))[t] = make_uint2(first, wm | (rel << 12));
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    if (lane == 63) wire_chunk_base(wire, g)[chunk] = total;  // chunk total, scanned later
+    // segments: this row's residuals of channel c = bytes [ry*w, ry*w + w) of the segment
+    if (wm & 0xfffu) {
+        unsigned char* seg = (unsigned char*)(stage + (size_t)t * STAGE_WORDS);
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            const uint32_t w = (mj >> (4 * c)) & 15u;
-            if (w == 0) continue;
-            pack_segment(seg, (z[j] >> (16 - 8 * c)) & 0xffu, w, lane);
-            seg += 2 * w;
+            const uint32_t w = (wm >> (4 * c)) & 15u;
+            const int sh = 16 - 8 * c;
+            uint32_t lo = 0, hi = 0;
+#pragma unroll
+            for (int rx = 0; rx < 8; ++rx) {
+                const uint32_t v = (z[rx] >> sh) & 0xffu, pos = (uint32_t)rx * w;
+                if (pos < 32) lo |= v << pos;
+                else hi |= v << (pos - 32);
+            }
+            unsigned char* dst = seg + ry * w;
+            if (w == 8) *(uint2*)dst = make_uint2(lo, hi);
+            else if (w == 4) *(uint32_t*)dst = lo;
+            else if (w == 2) *(uint16_t*)dst = (uint16_t)lo;
+            else if (w == 1) *dst = (unsigned char)lo;
+            seg += 8 * w;
         }
     }
-    return (uint32_t)__builtin_amdgcn_readlane((int)incl, CODEC_TPW - 1);
+    return total;
 }
 
 // Workgroup b owns the contiguous chunks [b * per, (b + 1) * per) (its waves take every 4th),
@@ -268,7 +204,7 @@ __global__ __launch_bounds__(256) void encode_tiles_kernel(const int32_t* __rest
     const int lane = threadIdx.x & 63, wave = wave_index();
     const int lo = blockIdx.x * per, hi = min(g.n_chunks, lo + per);
     uint32_t mine = 0;
-    for (int chunk = lo + wave; chunk < hi; chunk += 4) mine += encode_chunk(bands, wire, stage, g, chunk, lane);
+    for (int chunk = lo + wave; chunk < hi; chunk += 4) mine += encode_group(bands, wire, stage, g, chunk, lane);
     if (lane == 0) s_tot[wave] = mine;
     __syncthreads();
     if (threadIdx.x == 0) wg_total[blockIdx.x] = s_tot[0] + s_tot[1] + s_tot[2] + s_tot[3];
@@ -292,31 +228,28 @@ __device__ __forceinline__ uint32_t block_scan256(uint32_t x, uint32_t* s, uint3
     return r;
 }
 
-__device__ __forceinline__ void copy_chunk(const uint32_t* __restrict__ stage, unsigned char* __restrict__ wire,
+// One chunk's staged segments -> compact payload: lane 8j + q moves units q, q+8, q+16 of
+// tile t0 + j (loads first, then stores).
+__device__ __forceinline__ void copy_group(const uint64_t* __restrict__ stage, unsigned char* __restrict__ wire,
                                            const CodecGeom& g, int chunk, uint32_t base, int lane) {
-    const int t0 = chunk * CODEC_TPW;
-    const bool hv = lane < CODEC_TPW && t0 + lane < g.n_tiles;
-    const uint32_t meta = hv ? wire_tile_hdr(wire)[2 * (size_t)(t0 + lane) + 1] : 0u;
-    uint32_t* pay = (uint32_t*)wire_payload(wire, g);
-    uint32_t words[CODEC_TPW];
+    const int t = chunk * CODEC_TPW + (lane >> 3), q = lane & 7;
+    const bool live = t < g.n_tiles;
+    const uint32_t meta = live ? wire_tile_hdr(wire)[2 * (size_t)t + 1] : 0u;
+    const uint32_t u = units_of(meta);
+    uint64_t* pay = wire_payload(wire, g);
+    uint64_t v[3];
 #pragma unroll
-    for (int j = 0; j < CODEC_TPW; ++j) {  // non-flat tiles only; words past a tile's units are unused
-        const uint32_t mj = (uint32_t)__builtin_amdgcn_readlane((int)meta, j);
-        words[j] = 0u;
-        if (mj & 0xfffu) words[j] = stage[(size_t)(t0 + j) * STAGE_WORDS + min(lane, STAGE_WORDS - 1)];
-    }
+    for (int k = 0; k < 3; ++k) v[k] = q + 8 * k < (int)u ? stage[(size_t)t * STAGE_UNITS + q + 8 * k] : 0ull;
 #pragma unroll
-    for (int j = 0; j < CODEC_TPW; ++j) {
-        const uint32_t mj = (uint32_t)__builtin_amdgcn_readlane((int)meta, j);
-        if (lane < 2 * (int)units_of(mj)) pay[2 * ((size_t)base + (mj >> 12)) + lane] = words[j];
-    }
+    for (int k = 0; k < 3; ++k)
+        if (q + 8 * k < (int)u) pay[(size_t)base + (meta >> 12) + q + 8 * k] = v[k];
 }
 
 // Same workgroup ranges as encode_tiles_kernel: the base of workgroup b's chunks is the sum of
 // wg_total[0..b); its chunk totals (in chunk_base[]) are scanned in LDS and replaced by their
-// bases; then the staged segments move to their compact offsets (one wave per chunk, word q
-// of a tile by lane q).  The last workgroup writes the wire header and size.
-__global__ __launch_bounds__(256) void encode_copy_kernel(const uint32_t* __restrict__ stage,
+// bases; then the staged segments move to their compact offsets.  The last workgroup writes
+// the wire header and size.
+__global__ __launch_bounds__(256) void encode_copy_kernel(const uint64_t* __restrict__ stage,
                                                          unsigned char* __restrict__ wire,
                                                          const uint32_t* __restrict__ wg_total, CodecGeom g, int per,
                                                          int64_t* __restrict__ wire_bytes) {
@@ -341,7 +274,7 @@ __global__ __launch_bounds__(256) void encode_copy_kernel(const uint32_t* __rest
     }
     __syncthreads();
     for (int c = lo + tid; c < hi; c += 256) cb[c] = s_base[c - lo];
-    for (int chunk = lo + wave; chunk < hi; chunk += 4) copy_chunk(stage, wire, g, chunk, s_base[chunk - lo], lane);
+    for (int chunk = lo + wave; chunk < hi; chunk += 4) copy_group(stage, wire, g, chunk, s_base[chunk - lo], lane);
     if (b == (int)gridDim.x - 1 && tid == 0) {
         const uint32_t total = run;
         uint32_t* h = (uint32_t*)wire;
@@ -355,78 +288,89 @@ __global__ __launch_bounds__(256) void encode_copy_kernel(const uint32_t* __rest
     }
 }
 
-__device__ __forceinline__ void decode_chunk(const unsigned char* __restrict__ gathered, size_t rank_stride,
-                                             int32_t* __restrict__ frames, const CodecGeom& g, size_t gw, int lane) {
-    const int rank = (int)(gw / (size_t)g.n_chunks);
-    const int chunk = (int)(gw - (size_t)rank * g.n_chunks);
-    const int t0 = chunk * CODEC_TPW;
+// Decoder layout: lane L = 8 j + ry handles row ry (8 pixels) of tile t0 + j, so a row's
+// residuals of one channel are the w consecutive bytes [ry*w, ry*w + w) of the segment (one
+// aligned 8-byte load), the prefix along the row runs in registers, and the first column
+// needs only the lane above (DPP row shift by one).  A wave decodes one chunk.
+constexpr int DEC_TPW = CODEC_TPW;
+
+__device__ __forceinline__ void decode_group(const unsigned char* __restrict__ gathered, size_t rank_stride,
+                                             int32_t* __restrict__ frames, const CodecGeom& g, int groups, size_t gw,
+                                             int lane) {
+    const int rank = (int)(gw / (size_t)groups);
+    const int t0 = (int)(gw - (size_t)rank * groups) * DEC_TPW;
     const unsigned char* wire = gathered + (size_t)rank * rank_stride;
     const int total_bands = (g.H + g.band_rows - 1) / g.band_rows;
     const int nb = rank < total_bands ? (total_bands - 1 - rank) / g.world + 1 : 0;
-    const TileInfo ti = tile_info(g, rank, nb, t0 + (lane & (CODEC_TPW - 1)));
-    const bool hv = lane < CODEC_TPW && ti.live;
-    const uint2 hdr = hv ? ((const uint2*)wire_tile_hdr(wire))[t0 + lane] : make_uint2(0u, 0u);
-    const uint32_t base = wire_chunk_base(wire, g)[chunk];
-    const uint32_t* pay = (const uint32_t*)wire_payload(wire, g);
-    uint32_t words[CODEC_TPW];
+    const int j = lane >> 3, ry = lane & 7;
+    const int t = t0 + j;
+    const bool live = t < g.n_tiles;
+    const uint2 hdr = ((const uint2*)wire_tile_hdr(wire))[live ? t : 0];
+    const uint32_t first = live ? hdr.x : 0u, meta = live ? hdr.y : 0u;
+    const uint32_t base = wire_chunk_base(wire, g)[t0 / CODEC_TPW];  // the wave's chunk
+    const TilePos tp = tile_pos(g, t0, j);
+    const int f = tp.f, tr = tp.tr, tc = tp.tc;
+    const int r = tr * 8 + ry;
+    const int y = frame_row(g, rank, r);
+    const bool row_ok = live && r < nb * g.band_rows && y < g.H;
+    const int x0 = tc * 8;
+    // residual bytes of this row, channel by channel (width 0: nothing loaded, zeros)
+    const uint32_t w[3] = {meta & 15u, (meta >> 4) & 15u, (meta >> 8) & 15u};
+    const uint64_t* pay = wire_payload(wire, g);
+    uint32_t d[8];
 #pragma unroll
-    for (int j = 0; j < CODEC_TPW; ++j) {  // lanes past a tile's words read something harmless
-        const uint32_t mj = (uint32_t)__builtin_amdgcn_readlane((int)hdr.y, j);
-        const uint32_t nw = 2 * units_of(mj);
-        words[j] = nw ? pay[2 * ((size_t)base + (mj >> 12)) + min((uint32_t)lane, nw - 1)] : *(const uint32_t*)wire;
-    }
-    const int rx = lane & 7;
+    for (int i = 0; i < 8; ++i) d[i] = 0u;
+    if (__builtin_amdgcn_ballot_w64((meta & 0xfffu) != 0) != 0) {  // some tile of the wave is not flat
+        uint32_t seg = base + (meta >> 12);  // unit offset of the channel's segment
 #pragma unroll
-    for (int j = 0; j < CODEC_TPW; ++j) {
-        const uint32_t first = (uint32_t)__builtin_amdgcn_readlane((int)hdr.x, j);
-        const uint32_t mj = (uint32_t)__builtin_amdgcn_readlane((int)hdr.y, j);
-        int64_t row_off;
-        const bool inside = pixel_inside(g, rank, nb, ti, j, lane, &row_off);
-        uint32_t px = first;  // flat tile: every pixel is the first one
-        if (mj & 0xfffu) {    // wave-uniform
-            uint32_t zz = 0;
-            int wo = 0;  // word offset of the segment inside the tile's payload
+        for (int c = 0; c < 3; ++c) {
+            const uint32_t wc = w[c];
+            const uint32_t byte = (uint32_t)ry * wc;  // row's first byte inside the segment
+            const uint64_t* src = wc ? pay + seg + (byte >> 3) : (const uint64_t*)wire;
+            const uint64_t bits = wc ? (*src >> (8 * (byte & 7))) : 0ull;
+            const uint32_t lo = (uint32_t)bits, hi = (uint32_t)(bits >> 32);
+            const uint32_t mask = (1u << wc) - 1u;
 #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                const int w = (int)((mj >> (4 * c)) & 15u);
-                if (w == 0) continue;
-                const int pos = lane * w;
-                const uint32_t word = (uint32_t)__builtin_amdgcn_ds_bpermute((wo + (pos >> 5)) << 2, (int)words[j]);
-                zz |= ((word >> (pos & 31)) & ((1u << w) - 1u)) << (16 - 8 * c);
-                wo += 2 * w;
+            for (int rx = 0; rx < 8; ++rx) {
+                const uint32_t pos = (uint32_t)rx * wc;
+                const uint32_t word = pos < 32 ? lo : hi;
+                d[rx] |= ((word >> (pos & 31)) & mask) << (16 - 8 * c);
             }
-            const uint32_t d = unzigzag_bytes(zz) & 0xffffffu;
-            // first column: odd rows add the row above's residual, every row adds `first`
-            const uint32_t above = row_shr<8>(d);
-            const uint32_t col = add_bytes(first, (lane & 8) ? add_bytes(d, above) : d);
-            // rows: inclusive prefix inside each 8-lane row, seeded by the first column
-            uint32_t v = rx == 0 ? col : d;
-            uint32_t o = row_shr<1>(v);
-            if (rx >= 1) v = add_bytes(v, o);
-            o = row_shr<2>(v);
-            if (rx >= 2) v = add_bytes(v, o);
-            o = row_shr<4>(v);
-            if (rx >= 4) v = add_bytes(v, o);
-            px = v & 0xffffffu;
+            seg += wc;
         }
-        if (inside) frames[readlane64(ti.dst, j) + row_off + rx] = (int32_t)px;
+#pragma unroll
+        for (int rx = 0; rx < 8; ++rx) d[rx] = unzigzag_bytes(d[rx]) & 0xffffffu;
+    }
+    // first column: pixel (0, ry) = first + d0(ry) (+ d0(ry - 1) in odd rows, from the lane above)
+    const uint32_t d0_above = row_shr<1>(d[0]);
+    uint32_t px[8];
+    px[0] = add_bytes(first, (ry & 1) ? add_bytes(d[0], d0_above) : d[0]) & 0xffffffu;
+#pragma unroll
+    for (int rx = 1; rx < 8; ++rx) px[rx] = add_bytes(px[rx - 1], d[rx]) & 0xffffffu;
+    if (!row_ok) return;
+    int32_t* dst = frames + (size_t)f * g.frame_stride + (size_t)y * (size_t)g.W + (size_t)x0;
+    if (x0 + 8 <= g.W && ((uintptr_t)dst & 15) == 0) {
+        ((int4*)dst)[0] = make_int4((int)px[0], (int)px[1], (int)px[2], (int)px[3]);
+        ((int4*)dst)[1] = make_int4((int)px[4], (int)px[5], (int)px[6], (int)px[7]);
+    } else {
+#pragma unroll
+        for (int rx = 0; rx < 8; ++rx)
+            if (x0 + rx < g.W) dst[rx] = (int32_t)px[rx];
     }
 }
 
 // Decode every rank's wire (rank r's at gathered + r * rank_stride) of a batch into the
-// frames (frame f at frames + f * frame_stride).  One wave per chunk (CODEC_TPW tiles of one
-// rank): one load of their headers, one load of each tile's payload words (lane q: word q),
-// then per tile each lane fetches the word holding its bits (ds_bpermute), shifts and masks;
-// prefix sums by DPP; one store.  Flat tiles store their first pixel.
+// frames (frame f at frames + f * frame_stride): a resident grid of 4-wave workgroups walks
+// the (rank, 8-tile group) pairs.
 __global__ __launch_bounds__(256) void decode_tiles_kernel(const unsigned char* __restrict__ gathered,
                                                           size_t rank_stride, int32_t* __restrict__ frames,
                                                           CodecGeom g) {
     const int lane = threadIdx.x & 63;
-    const size_t n = (size_t)g.world * (size_t)g.n_chunks;
+    const int groups = (g.n_tiles + DEC_TPW - 1) / DEC_TPW;  // per rank
+    const size_t n = (size_t)g.world * (size_t)groups;
     for (size_t gw = (size_t)blockIdx.x * 4 + wave_index(); gw < n; gw += (size_t)gridDim.x * 4)
-        decode_chunk(gathered, rank_stride, frames, g, gw, lane);
+        decode_group(gathered, rank_stride, frames, g, groups, gw, lane);
 }
-
 
 int launch_encode_bands(const int32_t* bands, unsigned char* wire, const CodecGeom& g, int64_t* wire_bytes,
                         void* stage, void* stream) {
@@ -440,7 +384,7 @@ int launch_encode_bands(const int32_t* bands, unsigned char* wire, const CodecGe
     uint32_t* st = (uint32_t*)stage;
     uint32_t* wg_total = st + (size_t)g.n_chunks * CODEC_TPW * STAGE_WORDS;
     hipLaunchKernelGGL(encode_tiles_kernel, dim3((unsigned)blocks), dim3(256), 0, s, bands, wire, st, wg_total, g, per);
-    hipLaunchKernelGGL(encode_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const uint32_t*)st, wire,
+    hipLaunchKernelGGL(encode_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const uint64_t*)st, wire,
                        (const uint32_t*)wg_total, g, per, wire_bytes);
     return (int)hipGetLastError();
 }
@@ -454,7 +398,7 @@ size_t encode_stage_bytes(const CodecGeom& g) {
 
 int launch_decode_gathered(const unsigned char* gathered, size_t rank_stride, int32_t* frames, const CodecGeom& g,
                            void* stream) {
-    const size_t waves = (size_t)g.world * (size_t)g.n_chunks;
+    const size_t waves = (size_t)g.world * (size_t)((g.n_tiles + DEC_TPW - 1) / DEC_TPW);
     if (waves == 0) return (int)hipSuccess;
     hipLaunchKernelGGL(decode_tiles_kernel, dim3((unsigned)std::min<size_t>((waves + 3) / 4, CODEC_BLOCKS)), dim3(256), 0,
                        (hipStream_t)stream,

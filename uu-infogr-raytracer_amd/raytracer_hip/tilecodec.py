@@ -22,7 +22,7 @@ band sets before the gather and rank 0 decodes them straight into the frame:
   64 * w_c bits, lane l's residual at bits [l*w_c, (l+1)*w_c) of the little-endian stream
   (inside one 32-bit word, since w_c divides 32): the GPU packs a word with a DPP OR over
   32 / w_c lanes and unpacks a lane with one load, a shift and a mask.
-* Tiles are grouped in chunks of 16 consecutive tiles (one wave's tiles on the GPU); a
+* Tiles are grouped in chunks of 8 consecutive tiles (one wave's tiles on the GPU); a
   tile's payload offset is its chunk's base (a 32-bit unit offset, one per chunk) plus its
   offset inside the chunk (kept in the header).  Segments follow each other R, G, B.
 
@@ -47,7 +47,7 @@ TILE = 8
 _L = np.arange(64)
 # predictor lane of every lane: left; first column: above (odd rows) or lane 0 (even rows)
 PRED_SRC = np.where(_L % 8 > 0, _L - 1, np.where((_L // 8) % 2 == 1, _L - 8, 0))
-CHUNK = 16
+CHUNK = 8
 HEADER_BYTES = 16
 MAX_UNITS_PER_TILE = 24
 
