@@ -44,11 +44,14 @@ def parse():
                          "slot; every frame is fully traced)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="N>1: gather each frame before tracing the next (no double buffering)")
-    ap.add_argument("--batch", type=int, default=8,
-                    help="N>1: frames per RCCL gather (double-buffered; 1 = one gather per frame)")
+    ap.add_argument("--batch", type=int, default=16,
+                    help="N>1: frames per RCCL gather (pipelined; 1 = one gather per frame)")
     ap.add_argument("--band-format", choices=["tiles", "rgb24", "int32"], default="tiles",
                     help="N>1: band sets shipped to rank 0 tile-encoded (lossless, rt_encode_bands), as packed "
                          "24-bit RGB or as int32 pixels")
+    ap.add_argument("--rank0-codec", action="store_true",
+                    help="N>1 tiles: rank 0 encodes and decodes its own bands too (instead of rendering them "
+                         "straight into its frames); the one-process rehearsal uses it to exercise the codec")
     ap.add_argument("--dist-path", action="store_true",
                     help="rehearsal: run the N>1 band/gather path even with one process (RCCL world of 1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -179,21 +182,26 @@ def main():
                 ctx.encode_bands(W, H, rb.band_rows, rank, world, raw.data_ptr(), rb.slot_elems, n, wire.data_ptr(),
                                  size.data_ptr(), st.cuda_stream)
 
-            def t_decode(recv, rank_stride, n, frames_, st):
+            def t_decode(recv, rank_stride, n, frames_, st, first_rank):
                 ctx.decode_gathered(W, H, rb.band_rows, world, recv.data_ptr(), rank_stride, n, frames_.data_ptr(),
-                                    W * H, st.cuda_stream)
+                                    W * H, st.cuda_stream, first_rank=first_rank)
 
             tg = TileBandGather(rb, torch.device("cuda", local), args.batch,
-                                lambda n: wire_layout(W, H, rb.band_rows, world, n), t_encode, t_decode)
+                                lambda n: wire_layout(W, H, rb.band_rows, world, n), t_encode, t_decode,
+                                rank0_codec=args.rank0_codec)
+            out_fmt = abi.RT_BANDS_FRAME if tg.direct else abi.RT_BANDS_INT32
             # frames alternate between trace streams (two in flight per rank); at a batch end the
             # encode runs on `stream` after the others joined it, and the trace streams then wait
             # for it (the next-but-one batch reuses the raw buffer); collectives are waited on
-            # the gather's own side streams, never on a trace stream
+            # the gather's own side streams, never on a trace stream.  Rank 0 renders its own
+            # bands straight into its frame ring (RT_BANDS_FRAME): they never cross xGMI
             tstreams = [stream] + [torch.cuda.Stream() for _ in range(max(1, args.inflight) - 1)]
 
             def step():
                 k = tg.k
-                ctx.render_bands_ex(W, H, rb.band_rows, rank, world, tg.raw_frame().data_ptr(), abi.RT_BANDS_INT32,
+                if k % tg.F == 0:
+                    tg.begin_batch(tstreams)
+                ctx.render_bands_ex(W, H, rb.band_rows, rank, world, tg.target().data_ptr(), out_fmt,
                                     tstreams[k % len(tstreams)].cuda_stream)
                 end = (k + 1) % tg.F == 0
                 if end:

@@ -198,8 +198,10 @@ int rt_scatter_bands(rt_ctx* ctx, int width, int height, int band_rows, int band
 
 /* Band sets for shipping to rank 0.  Formats: RT_BANDS_INT32 (as
  * rt_render_bands) or RT_BANDS_RGB24 (3 bytes B, G, R per pixel: the top byte of
- * 0x00RRGGBB is always 0, so a quarter fewer bytes cross xGMI). */
-enum { RT_BANDS_INT32 = 0, RT_BANDS_RGB24 = 1 };
+ * 0x00RRGGBB is always 0, so a quarter fewer bytes cross xGMI), or RT_BANDS_FRAME: the
+ * bands straight into their rows of the row-major frame d_out[height][width] (other rows
+ * untouched) -- rank 0's own share, which never travels. */
+enum { RT_BANDS_INT32 = 0, RT_BANDS_RGB24 = 1, RT_BANDS_FRAME = 2 };
 int rt_render_bands_ex(rt_ctx* ctx, int width, int height, int band_rows, int band_first,
                        int band_step, void* d_out, int format, void* hip_stream, int* out_n_bands);
 /* Reassemble the band sets of `world` ranks (band b rendered by rank b % world with
@@ -232,10 +234,11 @@ int rt_wire_layout_of(int width, int height, int band_rows, int world, int n_fra
 int rt_encode_bands(rt_ctx* ctx, int width, int height, int band_rows, int rank, int world,
                     const int32_t* d_bands, size_t frame_stride, int n_frames, void* d_wire,
                     int64_t* d_wire_bytes, void* hip_stream);
-/* Decode the wires of all `world` ranks (rank r's at d_gathered + r * rank_stride, 8-aligned)
- * into frame f = d_frames + f * frame_stride (int32, row-major) for f < n_frames.  One
- * launch, asynchronous on hip_stream. */
-int rt_decode_gathered(rt_ctx* ctx, int width, int height, int band_rows, int world,
+/* Decode the wires of ranks first_rank .. world-1 (rank r's at d_gathered + r * rank_stride,
+ * 8-aligned; each region at least max_bytes) into frame f = d_frames + f * frame_stride
+ * (int32, row-major) for f < n_frames: only those ranks' rows are written (first_rank = 1:
+ * rank 0 rendered its own rows with RT_BANDS_FRAME).  One launch, asynchronous on hip_stream. */
+int rt_decode_gathered(rt_ctx* ctx, int width, int height, int band_rows, int world, int first_rank,
                        const void* d_gathered, size_t rank_stride, int n_frames, int32_t* d_frames,
                        size_t frame_stride, void* hip_stream);
 

@@ -156,7 +156,7 @@ def run_batched(rank, world, port, cfg, width, height, band_rows, frames, per_ba
         dist.destroy_process_group()
 
 
-def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batch, result_path):
+def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batch, result_path, rank0_codec=False):
     """bench.py's default N>1 step: F frames per batch, tile-encoded band sets (host mirror of
     rt_encode_bands), size all_reduce + gather, rank 0 decodes every frame (host mirror of
     rt_decode_gathered) and checks it against the oracle."""
@@ -192,25 +192,36 @@ def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batc
 
         decoded = [0]
 
-        def decode(recv, rank_stride, n, frames_, _stream):
+        def decode(recv, rank_stride, n, frames_, _stream, first_rank):
             host = recv.numpy()
             fr = frames_.numpy().reshape(-1, height, width)
-            fr[:] = -7
-            for r in range(world):
+            for r in range(first_rank, world):
                 tilecodec.decode_into(fr[:n], host[r * rank_stride:(r + 1) * rank_stride], width, height,
                                       band_rows, r, world)
             for f in range(n):
                 got[decoded[0] + f] = fr[f].copy()
+                fr[f] = -7  # the ring slot is reused: stale pixels must not pass
             decoded[0] += n
 
         g = TileBandGather(rb, "cpu", per_batch, lambda n: tilecodec.layout(width, height, band_rows, world, n),
-                           encode, decode)
+                           encode, decode, rank0_codec=rank0_codec)
+        if rank == 0:
+            for ring in g.frames:
+                ring.fill_(-7)
         for k in range(frames):
-            raw = g.raw_frame().numpy()
-            raw[:] = 0x5A5A5A  # rows this rank does not own must not leak into the frame
-            for l0, y0, n in rb.row_spans():
-                rows, _ = pyoracle.render(scene_for(k), pyoracle.MODE_NEAREST, 2, rows=(y0, y0 + n))
-                raw[l0 * width:(l0 + n) * width] = rows.reshape(-1)
+            if k % g.F == 0:
+                g.begin_batch()
+            dst = g.target().numpy()
+            if g.direct:  # rank 0 renders its bands into their frame rows
+                dst = dst.reshape(height, width)
+                for l0, y0, n in rb.row_spans():
+                    rows, _ = pyoracle.render(scene_for(k), pyoracle.MODE_NEAREST, 2, rows=(y0, y0 + n))
+                    dst[y0:y0 + n] = rows
+            else:
+                dst[:] = 0x5A5A5A  # rows this rank does not own must not leak into the frame
+                for l0, y0, n in rb.row_spans():
+                    rows, _ = pyoracle.render(scene_for(k), pyoracle.MODE_NEAREST, 2, rows=(y0, y0 + n))
+                    dst[l0 * width:(l0 + n) * width] = rows.reshape(-1)
             g.commit()
         g.drain()
         if rank == 0:

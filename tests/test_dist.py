@@ -126,8 +126,9 @@ def test_scatter_gathered_host_matches_scatter_host():
         assert np.array_equal(scatter_gathered_host(buf, stride, W, H, br, world, bpp), frame)
 
 
-@pytest.mark.parametrize("world,frames,per_batch", [(2, 7, 3), (3, 5, 2), (2, 9, 2)])
-def test_gloo_tile_encoded_gather(tmp_path, world, frames, per_batch):
+@pytest.mark.parametrize("world,frames,per_batch,rank0_codec", [(2, 7, 3, False), (3, 5, 2, False), (2, 9, 2, False),
+                                                               (3, 7, 3, True)])
+def test_gloo_tile_encoded_gather(tmp_path, world, frames, per_batch, rank0_codec):
     """bench.py's default N>1 step: tile-encoded band sets, size all_reduce + gather, three-stage
     pipeline; every frame decodes to its own oracle frame, the last batch may be partial."""
     import dist_worker
@@ -135,7 +136,8 @@ def test_gloo_tile_encoded_gather(tmp_path, world, frames, per_batch):
     port = _free_port()
     result = tmp_path / "result.txt"
     procs = [ctx.Process(target=dist_worker.run_tiles,
-                         args=(r, world, port, "C3", 43, 29, 4, frames, per_batch, str(result))) for r in range(world)]
+                         args=(r, world, port, "C3", 43, 29, 4, frames, per_batch, str(result), rank0_codec))
+             for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:

@@ -68,10 +68,13 @@ def test_device_wire_equals_host_mirror_and_decodes(gpu_ctx, kind, W, H, band_ro
     assert np.array_equal(out.cpu().numpy().reshape(F, H, W), frames)
 
 
-@pytest.mark.parametrize("cfg,world,band_rows", [("C2", 2, 8), ("C3", 8, 8), ("C4", 3, 8), ("REF", 5, 4)])
-def test_traced_band_sets_roundtrip_to_the_frame(gpu_ctx, cfg, world, band_rows):
+@pytest.mark.parametrize("cfg,world,band_rows,rank0_direct", [("C2", 2, 8, True), ("C3", 8, 8, True), ("C4", 3, 8, False),
+                                                              ("REF", 5, 4, True), ("C2", 1, 8, False)])
+def test_traced_band_sets_roundtrip_to_the_frame(gpu_ctx, cfg, world, band_rows, rank0_direct):
     """The N>1 data path on one GPU: every simulated rank traces its band set (rt_render_bands),
-    encodes it, rank 0 decodes all wires -> identical to the single-launch frame."""
+    encodes it, rank 0 decodes all wires -> identical to the single-launch frame.  With
+    rank0_direct, rank 0 renders its rows straight into the frame (RT_BANDS_FRAME) and the
+    decode starts at rank 1 (bench.py's default)."""
     import torch
     from raytracer_hip import abi
     sc = scenes.config(cfg)
@@ -85,7 +88,11 @@ def test_traced_band_sets_roundtrip_to_the_frame(gpu_ctx, cfg, world, band_rows)
     gathered = torch.zeros(world * stride, dtype=torch.uint8, device="cuda")
     s = torch.cuda.current_stream().cuda_stream
     total = 0
-    for r in range(world):
+    frame = torch.full((W * H,), -1, dtype=torch.int32, device="cuda")
+    first = 1 if rank0_direct else 0
+    if rank0_direct:
+        gpu_ctx.render_bands_ex(W, H, band_rows, 0, world, frame.data_ptr(), abi.RT_BANDS_FRAME, s)
+    for r in range(first, world):
         rb = RowBands(W, H, band_rows, r, world)
         buf = torch.zeros(rb.slot_elems, dtype=torch.int32, device="cuda")
         gpu_ctx.render_bands_ex(W, H, band_rows, r, world, buf.data_ptr(), abi.RT_BANDS_INT32, s)
@@ -94,8 +101,8 @@ def test_traced_band_sets_roundtrip_to_the_frame(gpu_ctx, cfg, world, band_rows)
                              gathered[r * stride:].data_ptr(), size.data_ptr(), s)
         torch.cuda.synchronize()
         total += int(size.item())
-    frame = torch.full((W * H,), -1, dtype=torch.int32, device="cuda")
-    gpu_ctx.decode_gathered(W, H, band_rows, world, gathered.data_ptr(), stride, 1, frame.data_ptr(), W * H, s)
+    gpu_ctx.decode_gathered(W, H, band_rows, world, gathered.data_ptr(), stride, 1, frame.data_ptr(), W * H, s,
+                            first_rank=first)
     torch.cuda.synchronize()
     assert np.array_equal(frame.cpu().numpy().reshape(H, W), full)
     assert total < 3 * W * H  # smaller than the RGB24 band sets

@@ -706,7 +706,7 @@ int rt_render_bands_ex(rt_ctx* ctx, int width, int height, int band_rows, int ba
     int rc = check_ctx(ctx, width, height);
     if (rc != RT_OK) return rc;
     if (band_rows <= 0 || band_first < 0 || band_step <= 0 || !d_out ||
-        (format != RT_BANDS_INT32 && format != RT_BANDS_RGB24))
+        (format != RT_BANDS_INT32 && format != RT_BANDS_RGB24 && format != RT_BANDS_FRAME))
         return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_bands: bad band arguments");
     if (ctx->n_gpus != 1) return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_bands needs a single-GPU context");
     Device& d = ctx->dev[0];
@@ -807,14 +807,18 @@ int rt_encode_bands(rt_ctx* ctx, int width, int height, int band_rows, int rank,
     return RT_OK;
 }
 
-int rt_decode_gathered(rt_ctx* ctx, int width, int height, int band_rows, int world, const void* d_gathered,
-                       size_t rank_stride, int n_frames, int32_t* d_frames, size_t frame_stride, void* hip_stream) {
+int rt_decode_gathered(rt_ctx* ctx, int width, int height, int band_rows, int world, int first_rank,
+                       const void* d_gathered, size_t rank_stride, int n_frames, int32_t* d_frames,
+                       size_t frame_stride, void* hip_stream) {
     if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "NULL context");
     rtk::CodecGeom g;
-    if (!codec_geom(width, height, band_rows, world, n_frames, g, nullptr) || !d_gathered || !d_frames ||
-        ((uintptr_t)d_gathered & 7) != 0 || (rank_stride & 7) != 0 || (world > 1 && rank_stride < g.fixed_bytes) ||
-        frame_stride < (size_t)width * height)
+    rt_wire_layout lay;
+    if (!codec_geom(width, height, band_rows, world, n_frames, g, &lay) || !d_gathered || !d_frames ||
+        first_rank < 0 || first_rank > world || ((uintptr_t)d_gathered & 7) != 0 || (rank_stride & 7) != 0 ||
+        (world - first_rank > 1 && rank_stride < lay.max_bytes) || frame_stride < (size_t)width * height)
         return fail(ctx, RT_ERR_INVALID_ARG, "rt_decode_gathered: bad arguments");
+    if (first_rank == world) return RT_OK;
+    g.rank = first_rank;
     g.frame_stride = frame_stride;
     Device& d = ctx->dev[0];
     DeviceGuard guard(d.id);

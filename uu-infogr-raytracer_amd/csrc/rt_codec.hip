@@ -297,8 +297,9 @@ constexpr int DEC_TPW = CODEC_TPW;
 __device__ __forceinline__ void decode_group(const unsigned char* __restrict__ gathered, size_t rank_stride,
                                              int32_t* __restrict__ frames, const CodecGeom& g, int groups, size_t gw,
                                              int lane) {
-    const int rank = (int)(gw / (size_t)groups);
-    const int t0 = (int)(gw - (size_t)rank * groups) * DEC_TPW;
+    const int rel_rank = (int)(gw / (size_t)groups);
+    const int t0 = (int)(gw - (size_t)rel_rank * groups) * DEC_TPW;
+    const int rank = g.rank + rel_rank;
     const unsigned char* wire = gathered + (size_t)rank * rank_stride;
     const int total_bands = (g.H + g.band_rows - 1) / g.band_rows;
     const int nb = rank < total_bands ? (total_bands - 1 - rank) / g.world + 1 : 0;
@@ -359,15 +360,15 @@ __device__ __forceinline__ void decode_group(const unsigned char* __restrict__ g
     }
 }
 
-// Decode every rank's wire (rank r's at gathered + r * rank_stride) of a batch into the
-// frames (frame f at frames + f * frame_stride): a resident grid of 4-wave workgroups walks
-// the (rank, 8-tile group) pairs.
+// Decode the wires of ranks g.rank .. world-1 (rank r's at gathered + r * rank_stride) of a
+// batch into the frames (frame f at frames + f * frame_stride): a resident grid of 4-wave
+// workgroups walks the (rank, 8-tile group) pairs.
 __global__ __launch_bounds__(256) void decode_tiles_kernel(const unsigned char* __restrict__ gathered,
                                                           size_t rank_stride, int32_t* __restrict__ frames,
                                                           CodecGeom g) {
     const int lane = threadIdx.x & 63;
     const int groups = (g.n_tiles + DEC_TPW - 1) / DEC_TPW;  // per rank
-    const size_t n = (size_t)g.world * (size_t)groups;
+    const size_t n = (size_t)(g.world - g.rank) * (size_t)groups;  // ranks g.rank .. world-1
     for (size_t gw = (size_t)blockIdx.x * 4 + wave_index(); gw < n; gw += (size_t)gridDim.x * 4)
         decode_group(gathered, rank_stride, frames, g, groups, gw, lane);
 }
@@ -398,7 +399,7 @@ size_t encode_stage_bytes(const CodecGeom& g) {
 
 int launch_decode_gathered(const unsigned char* gathered, size_t rank_stride, int32_t* frames, const CodecGeom& g,
                            void* stream) {
-    const size_t waves = (size_t)g.world * (size_t)((g.n_tiles + DEC_TPW - 1) / DEC_TPW);
+    const size_t waves = (size_t)(g.world - g.rank) * (size_t)((g.n_tiles + DEC_TPW - 1) / DEC_TPW);
     if (waves == 0) return (int)hipSuccess;
     hipLaunchKernelGGL(decode_tiles_kernel, dim3((unsigned)std::min<size_t>((waves + 3) / 4, CODEC_BLOCKS)), dim3(256), 0,
                        (hipStream_t)stream,

@@ -115,7 +115,7 @@ struct LaunchParams {
     // global row = band * band_rows + r % band_rows; pixel written at out[r * W + x].
     int band_rows, band_first, band_step, local_rows;
     int32_t* out;
-    int out_fmt;  // 0: int32 0x00RRGGBB per pixel; 1: packed 24-bit (bytes B, G, R) per pixel
+    int out_fmt;  // 0: int32 0x00RRGGBB per pixel; 1: packed 24-bit (bytes B, G, R); 2: int32 at frame row y
     unsigned long long* counters;  // COUNTER_SLOTS x {primary, reflect, shadow, pad}
     int prim_const;                // 1: pc[0..S) and pbox[0..S) valid (S <= MAX_PRIM_CONST)
     PrimConst pc[MAX_PRIM_CONST];
@@ -141,7 +141,7 @@ int launch_scatter_bands(const int32_t* bands, int32_t* frame, int W, int H, int
 
 // Band-set tile codec (rt_codec.hip; format: raytracer_hip/tilecodec.py).
 struct CodecGeom {
-    int W, H, band_rows, rank, world, n_bands;  // n_bands: bands of `rank` (encoder)
+    int W, H, band_rows, rank, world, n_bands;  // rank / n_bands: the encoder's rank; the decoder's first rank
     int tiles_x, tiles_y, tiles_per_frame, n_tiles, n_chunks;
     size_t frame_stride;  // elements between frames (input band sets / output frames)
     size_t fixed_bytes;   // wire: header + tile headers + chunk bases, 8-aligned

@@ -223,10 +223,13 @@ __device__ __forceinline__ uint32_t shift_channel(float c) {
     return (uint32_t)(int32_t)__builtin_floorf(cl * 255.0f);
 }
 
-// Frame / band output: int32 0x00RRGGBB, or packed 24-bit (B, G, R bytes; the top byte of
-// the int32 is always 0) for band sets shipped to rank 0 -- a quarter fewer bytes over xGMI.
-__device__ __forceinline__ void store_pixel(const LaunchParams& p, size_t i, uint32_t px32) {
-    if (p.out_fmt == 0) {
+// Frame / band output: int32 0x00RRGGBB at the packed band row r (format 0) or at the frame
+// row y (format 2), or packed 24-bit (B, G, R bytes; the top byte of the int32 is always 0)
+// for band sets shipped to rank 0 -- a quarter fewer bytes over xGMI (format 1).
+// Format 2 (RT_BANDS_FRAME): the rank's bands straight into the row-major frame (row y).
+__device__ __forceinline__ void store_pixel(const LaunchParams& p, int r, int y, int x, uint32_t px32) {
+    const size_t i = (size_t)(p.out_fmt == 2 ? y : r) * (size_t)p.W + (size_t)x;
+    if (p.out_fmt != 1) {
         p.out[i] = (int32_t)px32;
     } else {
         unsigned char* o = (unsigned char*)p.out + i * 3;
@@ -921,7 +924,7 @@ __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p
                               &cnt);
         }
         const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
-        store_pixel(p, (size_t)r * (size_t)p.W + (size_t)x, px32);
+        store_pixel(p, r, y, x, px32);
     }
 
     add_counters(p, lane, wave, valid ? 1u : 0u, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT);
@@ -1423,7 +1426,7 @@ __global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel(LaunchParams p
     }
     if (valid) {
         const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
-        store_pixel(p, (size_t)r * (size_t)p.W + (size_t)x, px32);
+        store_pixel(p, r, y, x, px32);
     }
 
     add_counters(p, lane, wave, valid ? 1u : 0u, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT);

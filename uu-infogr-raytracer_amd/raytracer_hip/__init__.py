@@ -162,9 +162,11 @@ class Context:
                                              C.c_void_p(d_wire_bytes or None), C.c_void_p(stream)))
 
     def decode_gathered(self, width: int, height: int, band_rows: int, world: int, d_gathered: int,
-                        rank_stride: int, n_frames: int, d_frames: int, frame_stride: int, stream: int = 0):
-        """Decode every rank's wire (rank r's at d_gathered + r * rank_stride) into the frames."""
-        self._check(self.lib.rt_decode_gathered(self.ptr, width, height, band_rows, world, C.c_void_p(d_gathered),
+                        rank_stride: int, n_frames: int, d_frames: int, frame_stride: int, stream: int = 0,
+                        first_rank: int = 0):
+        """Decode the wires of ranks first_rank.. (rank r's at d_gathered + r * rank_stride) into the frames."""
+        self._check(self.lib.rt_decode_gathered(self.ptr, width, height, band_rows, world, first_rank,
+                                                C.c_void_p(d_gathered),
                                                 rank_stride, n_frames, C.c_void_p(d_frames), frame_stride,
                                                 C.c_void_p(stream)))
 

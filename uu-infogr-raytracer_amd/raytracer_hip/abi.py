@@ -14,7 +14,7 @@ PKG_ROOT = os.path.dirname(_HERE)
 LIB_PATH = os.path.join(PKG_ROOT, "lib", "libraytracer_hip.so")
 
 RT_ABI_VERSION = 4  # include/raytracer_hip.h
-RT_BANDS_INT32, RT_BANDS_RGB24 = 0, 1
+RT_BANDS_INT32, RT_BANDS_RGB24, RT_BANDS_FRAME = 0, 1, 2
 RT_OK = 0
 RT_ERR_INVALID_ARG = -1
 RT_ERR_NO_DEVICE = -2
@@ -116,7 +116,7 @@ EXPORTS = [
     ("rt_wire_layout_of", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(rt_wire_layout)]),
     ("rt_encode_bands", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_size_t,
                                   C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
-    ("rt_decode_gathered", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_size_t,
+    ("rt_decode_gathered", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_size_t,
                                      C.c_int, C.c_void_p, C.c_size_t, C.c_void_p]),
     ("rt_render_async", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     ("rt_wait", C.c_int, [C.c_void_p]),

@@ -232,47 +232,59 @@ class TileBandGather:
     """Tile-encoded band sets, F frames per batch, three-stage pipeline (bench.py's N > 1 step).
 
     Rendered frames are mostly flat, so shipping them to rank 0 raw (3-4 bytes per pixel)
-    spends xGMI bandwidth on redundancy; each rank tile-encodes its batch (rt_encode_bands,
-    format in raytracer_hip/tilecodec.py) and rank 0 decodes every rank's wire straight into
-    its frames (rt_decode_gathered).  A wire's size varies with the image, and a gather moves
-    the same count from every rank, so each batch costs two collectives:
+    spends xGMI bandwidth on redundancy; each rank r > 0 tile-encodes its batch
+    (rt_encode_bands, format in raytracer_hip/tilecodec.py) and rank 0 decodes the other ranks'
+    wires straight into its frames (rt_decode_gathered, first_rank 1).  Rank 0 renders its own
+    bands directly into the frames (RT_BANDS_FRAME): they never travel, so it neither encodes
+    nor decodes them (`rank0_codec=True` routes them through the codec anyway -- the
+    one-process rehearsal uses that to exercise it).  A wire's size varies with the image, and
+    a gather moves the same count from every rank, so each batch costs two collectives:
 
         A  encode batch b into wire b % 3; all_reduce(MAX) of the wire sizes   (async)
         B  batch b-1: wait for its all_reduce, read the max size on the host, gather that
            many bytes of every rank's wire into rank 0's receive buffer (b-1) % 2  (async)
-        C  batch b-2 (rank 0): wait for its gather, decode all ranks' wires into the frames
+        C  batch b-2 (rank 0): wait for its gather, decode the wires into frame ring (b-2) % 3
 
     run at every batch boundary, so the host waits only for a size that was reduced one batch
     earlier while the GPU traces the current batch.  On GPUs the waits for collectives are put
     on two side streams (`comm`, `dec`), never on the trace streams; events order buffer reuse
     (wire b % 3 is re-encoded only after gather b completed, receive buffer b % 2 is
-    overwritten only after decode b).  With gloo on CPU tensors (tests) the same sequence runs
-    synchronously.
+    overwritten only after decode b, rank 0 renders batch b into frame ring b % 3 only after
+    decode b-3 filled it -- `begin_batch`).  With gloo on CPU tensors (tests) the same
+    sequence runs synchronously.
 
-        raw = g.raw_frame(k)       -> int32 tensor view: this rank's band set of frame k
-        g.commit(main_stream)      -> after frame k was traced (run stages at batch ends)
-        g.drain()                  -> submit a partial last batch and finish every stage
+        g.begin_batch(streams)      -> before frame k when k % F == 0 (rank 0: ring reuse)
+        dst = g.target(k)           -> rank 0 direct: int32 view of frame k's ring slot (render
+                                       its bands there, RT_BANDS_FRAME); else this rank's raw
+                                       band set of frame k (RT_BANDS_INT32)
+        g.commit(main_stream)       -> after frame k was traced (stages at batch ends)
+        g.drain()                   -> submit a partial last batch and finish every stage
     `encode(raw_batch, n_frames, wire, size_tensor, stream)` and
-    `decode(gathered, rank_stride, n_frames, frames, stream)` do the codec work (the HIP library
-    on GPUs, the host mirror in tests); `frames` (rank 0) holds F decoded frames.
+    `decode(gathered, rank_stride, n_frames, frames, stream, first_rank)` do the codec work (the
+    HIP library on GPUs, the host mirror in tests).  Rank 0's decoded frames of batch b are in
+    `frames[b % 3]` (F frames, row-major) once stage C of b has run (`ring_of`).
     """
 
-    def __init__(self, rb: RowBands, device, frames_per_batch, layout_fn, encode, decode):
+    def __init__(self, rb: RowBands, device, frames_per_batch, layout_fn, encode, decode, rank0_codec=False):
         import torch
         self.rb, self.F, self.device = rb, max(1, frames_per_batch), torch.device(device)
         self.cuda = self.device.type == "cuda"
         self.layout_fn, self.encode, self.decode = layout_fn, encode, decode
+        self.first_rank = 0 if rank0_codec else 1
+        self.direct = rb.rank == 0 and not rank0_codec  # rank 0 renders into its frames
         self.slot_elems = rb.slot_elems
         lay = layout_fn(self.F)
         self.rank_stride = (int(lay.max_bytes) + 255) // 256 * 256
-        self.raw = [torch.zeros(self.F * self.slot_elems, dtype=torch.int32, device=self.device) for _ in range(2)]
+        self.raw = ([torch.zeros(self.F * self.slot_elems, dtype=torch.int32, device=self.device) for _ in range(2)]
+                    if not self.direct else None)
         self.wire = [torch.zeros(self.rank_stride, dtype=torch.uint8, device=self.device) for _ in range(3)]
         self.size = [torch.zeros(1, dtype=torch.int64, device=self.device) for _ in range(3)]
         self.size_host = torch.zeros(3, dtype=torch.int64, pin_memory=self.cuda)
         self.recv = ([torch.zeros(rb.world * self.rank_stride, dtype=torch.uint8, device=self.device)
                       for _ in range(2)] if rb.rank == 0 else [None, None])
-        self.frames = (torch.zeros(self.F * rb.width * rb.height, dtype=torch.int32, device=self.device)
-                       if rb.rank == 0 else None)
+        self.frame_elems = rb.width * rb.height
+        self.frames = ([torch.zeros(self.F * self.frame_elems, dtype=torch.int32, device=self.device)
+                        for _ in range(3)] if rb.rank == 0 else None)
         if self.cuda:
             self.comm, self.dec = torch.cuda.Stream(self.device), torch.cuda.Stream(self.device)
         self.k = 0             # frames rendered
@@ -280,15 +292,36 @@ class TileBandGather:
         self.stage_b = []      # [(batch, n_frames, all_reduce work)]
         self.stage_c = []      # [(batch, n_frames, gather work)]
         self.gathered_ev = {}  # batch -> event after its gather (wire reusable)
-        self.decoded_ev = {}   # batch -> event after its decode (receive buffer reusable)
+        self.decoded_ev = {}   # batch -> event after its decode (receive buffer / frame ring reusable)
         self.decoded = 0       # batches decoded (rank 0)
         self.bytes_sent = 0    # wire bytes gathered per rank (sum over batches)
 
-    def raw_frame(self, k=None):
+    def ring_of(self, batch):
+        return self.frames[batch % 3]
+
+    def target(self, k=None):
         k = self.k if k is None else k
-        i = (k // self.F) % 2
+        if self.direct:
+            o = (k % self.F) * self.frame_elems
+            return self.frames[(k // self.F) % 3][o:o + self.frame_elems]
         o = (k % self.F) * self.slot_elems
-        return self.raw[i][o:o + self.slot_elems]
+        return self.raw[(k // self.F) % 2][o:o + self.slot_elems]
+
+    def raw_frame(self, k=None):  # (the band set of a rank that encodes)
+        return self.target(k)
+
+    def begin_batch(self, streams=()):
+        """Before the first frame of a batch: rank 0's frame ring of this batch was last filled
+        by the decode of batch b-3, which must finish before the ring is rendered into again."""
+        b = self.k // self.F
+        while self.stage_b and self.stage_b[0][0] <= b - 3:  # (no-ops in steady state)
+            self._stage_b()
+        while self.stage_c and self.stage_c[0][0] <= b - 3:
+            self._stage_c()
+        if self.direct and b - 3 in self.decoded_ev and self.cuda:
+            ev = self.decoded_ev[b - 3]
+            for st in streams:
+                st.wait_event(ev)
 
     # -- stages -------------------------------------------------------------------
     def _stage_a(self, main, n_frames):
@@ -303,11 +336,13 @@ class TileBandGather:
             ev = self.gathered_ev.pop(b - 3)
             if self.cuda:
                 main.wait_event(ev)
-        self.encode(self.raw[b % 2], n_frames, self.wire[i], self.size[i], main)
+        if self.direct:
+            self.size[i].zero_()  # nothing to ship: rank 0's bands are already in its frames
+        else:
+            self.encode(self.raw[b % 2], n_frames, self.wire[i], self.size[i], main)
         work = dist.all_reduce(self.size[i], op=dist.ReduceOp.MAX, async_op=True)
         self.stage_b.append((b, n_frames, work))
         self.batch += 1
-
     def _stage_b(self):
         import torch
         import torch.distributed as dist
@@ -336,7 +371,9 @@ class TileBandGather:
         if self.cuda:
             with torch.cuda.stream(self.comm):
                 if b - 2 in self.decoded_ev:  # receive buffer j was last read by decode b-2
-                    self.comm.wait_event(self.decoded_ev.pop(b - 2))
+                    self.comm.wait_event(self.decoded_ev[b - 2])
+                for old in [x for x in self.decoded_ev if x < b - 4]:
+                    del self.decoded_ev[old]
                 gw = dist.gather(self.wire[i][:n], glist, dst=0, async_op=True)
         else:
             gw = dist.gather(self.wire[i][:n], glist, dst=0, async_op=True)
@@ -352,7 +389,8 @@ class TileBandGather:
                 ev.record(self.dec)
                 self.gathered_ev[b] = ev
                 if self.rb.rank == 0:
-                    self.decode(self.recv[b % 2], self.rank_stride, n_frames, self.frames, self.dec)
+                    self.decode(self.recv[b % 2], self.rank_stride, n_frames, self.ring_of(b), self.dec,
+                                self.first_rank)
                     dv = torch.cuda.Event()
                     dv.record(self.dec)
                     self.decoded_ev[b] = dv
@@ -360,7 +398,7 @@ class TileBandGather:
             gw.wait()
             self.gathered_ev[b] = None
             if self.rb.rank == 0:
-                self.decode(self.recv[b % 2], self.rank_stride, n_frames, self.frames, None)
+                self.decode(self.recv[b % 2], self.rank_stride, n_frames, self.ring_of(b), None, self.first_rank)
                 self.decoded_ev[b] = None
         if self.rb.rank == 0:
             self.decoded += 1
