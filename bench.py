@@ -39,8 +39,11 @@ def parse():
                     help="untimed frames first: the GPU needs ~10 ms of load to reach steady clocks")
     ap.add_argument("--config", default="C2")
     ap.add_argument("--band-rows", type=int, default=8)
+    ap.add_argument("--frames-per-launch", type=int, default=16,
+                    help="N=1: frames traced per launch (rt_render_bands_batch; every frame in full, the same "
+                         "camera); 1 = one rt_render_device launch per frame.  N>1 tiles: = --batch")
     ap.add_argument("--inflight", type=int, default=2,
-                    help="N=1: frames in flight (a swap chain: one stream and one output buffer per frame "
+                    help="launches in flight (a swap chain: one stream and one output buffer per launch "
                          "slot; every frame is fully traced)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="N>1: gather each frame before tracing the next (no double buffering)")
@@ -56,6 +59,8 @@ def parse():
                     help="rehearsal: run the N>1 band/gather path even with one process (RCCL world of 1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-tick", action="store_true",
+                    help="skip the Tick()-path probe (profiling runs: keeps every trace dispatch the same size)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="rocprofv3 PMC summary (HBM bytes per trace launch) for roofline.traffic")
     return ap.parse_args()
@@ -141,11 +146,16 @@ def main():
 
     streams = [stream]
     tg = None  # tile-encoded gather (N > 1, --band-format tiles)
+    run = None  # run(n): n steps (frames); else one step() per frame
     if not distributed:
         nf = max(1, args.inflight)
-        frames = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in range(nf)]
+        fpl = max(1, args.frames_per_launch)
+        frames = [torch.empty(fpl * W * H, dtype=torch.int32, device="cuda") for _ in range(nf)]
+        fptr = [f.data_ptr() for f in frames]
         streams += [torch.cuda.Stream() for _ in range(nf - 1)]
-        px_per_launch = W * H
+        sptr = [st_.cuda_stream for st_ in streams]
+        launch_frames = fpl
+        px_per_launch = fpl * W * H
         k_step = [0]
 
         def step():
@@ -153,10 +163,23 @@ def main():
             # frame k's last waves finish
             k = k_step[0]
             k_step[0] = k + 1
-            ctx.render_device(W, H, frames[k % nf].data_ptr(), streams[k % nf].cuda_stream)
+            ctx.render_device(W, H, fptr[k % nf], sptr[k % nf])
+
+        if fpl > 1:
+            def run(n):  # noqa: F811
+                # launches of fpl frames (each traced in full into its own buffer slot), two
+                # launches in flight on the swap-chain streams
+                done = 0
+                while done < n:
+                    m = min(fpl, n - done)
+                    i = k_step[0] % nf
+                    k_step[0] += 1
+                    ctx.render_bands_batch(W, H, H, 0, 1, m, fptr[i], W * H * 4, abi.RT_BANDS_INT32, sptr[i])
+                    done += m
     else:
         from raytracer_hip.dist import BandGather, BatchedBandGather, RowBands
         rb = RowBands(W, H, args.band_rows, rank, world)
+        launch_frames = 1
         px_per_launch = rb.pixels
         frame = torch.empty(W * H, dtype=torch.int32, device="cuda") if rank == 0 else None
 
@@ -196,21 +219,34 @@ def main():
             # the gather's own side streams, never on a trace stream.  Rank 0 renders its own
             # bands straight into its frame ring (RT_BANDS_FRAME): they never cross xGMI
             tstreams = [stream] + [torch.cuda.Stream() for _ in range(max(1, args.inflight) - 1)]
+            stride_b = (W * H if tg.direct else rb.slot_elems) * 4
+            launch_frames = tg.F
+            px_per_launch = tg.F * rb.pixels
+            if rank == 0:
+                frame = None  # the decoded frames live in tg.frames (rings of F)
 
-            def step():
-                k = tg.k
-                if k % tg.F == 0:
-                    tg.begin_batch(tstreams)
-                ctx.render_bands_ex(W, H, rb.band_rows, rank, world, tg.target().data_ptr(), out_fmt,
-                                    tstreams[k % len(tstreams)].cuda_stream)
-                end = (k + 1) % tg.F == 0
-                if end:
-                    for t in tstreams[1:]:
-                        stream.wait_stream(t)
-                tg.commit(stream)
-                if end:
-                    for t in tstreams[1:]:
-                        t.wait_stream(stream)
+            def run(n):  # noqa: F811
+                # one launch per batch (F frames of this rank's bands, each in full; a rank's share
+                # of a 1080p frame is too little GPU work for a launch per frame), batches
+                # alternating between the trace streams; at a batch end the encode runs on
+                # `stream` after the batch's stream joined it, and that trace stream waits for it
+                # (the next-but-one batch reuses the raw buffer)
+                done = 0
+                while done < n:
+                    m = min(tg.F - tg.k % tg.F, n - done)
+                    ts = tstreams[(tg.k // tg.F) % len(tstreams)]
+                    if tg.k % tg.F == 0:
+                        tg.begin_batch([ts])
+                    ctx.render_bands_batch(W, H, rb.band_rows, rank, world, m, tg.target().data_ptr(), stride_b,
+                                           out_fmt, ts.cuda_stream)
+                    end = (tg.k + m) % tg.F == 0
+                    if end and ts is not stream:
+                        stream.wait_stream(ts)
+                    for _ in range(m):
+                        tg.commit(stream)
+                    if end and ts is not stream:
+                        ts.wait_stream(stream)
+                    done += m
 
             def finish():  # noqa: F811  -- the last (possibly partial) batch, every stage
                 for t in tstreams[1:]:
@@ -262,8 +298,14 @@ def main():
                 join_traces()
                 reassemble(bgb.drain())
 
-    for _ in range(args.warmup):
-        step()
+    if run is None:
+        def run(n):  # noqa: F811
+            for _ in range(n):
+                step()
+
+    if launch_frames > 1:
+        ctx.set_timing(4)  # launches of many frames: an event pair per 4 launches costs nothing
+    run(args.warmup)
     finish()
     torch.cuda.synchronize()
     ctx.reset_stats()
@@ -278,8 +320,8 @@ def main():
     ev0.record(stream)  # on the launch stream(s): the others start after it, it ends after them
     for st_ in streams[1:]:
         st_.wait_event(ev0)
-    for _ in range(args.steps):
-        step()
+    run(args.steps)
+    host_s = (time.perf_counter() - t0) / max(1, args.steps)  # host issue time per step (incl. any waits)
     finish()
     for st_ in streams[1:]:
         stream.wait_stream(st_)
@@ -311,9 +353,13 @@ def main():
         rays_per_frame = rays / steps
         achieved_gbs = 4.0 * px_per_launch / kernel_s / 1e9
         pmc = load_pmc(args.pmc, sc.name, world)
-        traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+        # PMC summaries are per dispatch of `frames_per_launch` frames (tools/pmc.sh): per frame,
+        # then per launch of this run
+        pmc_frames = (pmc.get("frames_per_launch") or 1) if pmc else 1
+        traffic = pmc["hbm_bytes_per_launch"] / pmc_frames * launch_frames if pmc else None
         valu_insts = (pmc.get("counters") or {}).get("SQ_INSTS_VALU") if pmc else None
-        brute_tops = (f_alg / steps / max(1, world)) / kernel_s / 1e12
+        valu_frame = valu_insts / pmc_frames if valu_insts else None  # wave instructions per frame
+        brute_tops = (f_alg / steps / max(1, world)) * launch_frames / kernel_s / 1e12
         out = {
             "metric": METRIC,
             "value": rays / elapsed / 1e6,
@@ -332,7 +378,8 @@ def main():
                 "workload": f"{sc.name}: {sc.note}",
                 "width": W, "height": H, "spheres": len(sc.spheres), "planes": len(sc.planes),
                 "lights": len(sc.lights), "depth": sc.recursion_limit + 1,
-                "parallelism": f"single GPU, {max(1, args.inflight)} frames in flight" if not distributed else
+                "parallelism": (f"single GPU, {max(1, args.frames_per_launch)} frames per launch, "
+                                f"{max(1, args.inflight)} launches in flight") if not distributed else
                 f"interleaved {args.band_rows}-row bands x {world} ranks + RCCL gather to rank 0"
                 + (" (one gather per frame)" if args.no_pipeline else
                    f" ({args.batch} frames per gather, {args.band_format} bands, double-buffered: the gather of "
@@ -348,33 +395,39 @@ def main():
                 "traffic": traffic,
                 "kernel": "trace_direct_kernel" if sc and len(sc.spheres) < 12 else "trace_bundle_kernel",
                 "kernel_avg_ms": kernel_s * 1e3,
-                "kernel_avg_source": "sampled per-launch HIP event pairs (rt_set_timing, every 64th launch)",
+                "frames_per_launch": launch_frames,
+                "kernel_avg_source": "sampled per-launch HIP event pairs on the launch's stream (rt_set_timing: every "
+                                     "64th launch, every 4th for multi-frame launches)",
                 "frame_period_ms": period_s * 1e3,
-                "note": "algorithmic bytes = 4 B framebuffer store per pixel; the path is FP32-VALU-bound",
+                "note": "algorithmic bytes = 4 B framebuffer store per pixel x pixels per launch; the path is "
+                        "FP32-VALU-bound",
             },
             "roofline_valu": {
                 "bound": "valu",
                 # chip-level issue rate: SQ_INSTS_VALU (wave instructions per launch, PMC) x 64
                 # lanes per frame, over the frame period (frames overlap when several are in flight)
-                "achieved": valu_insts * 64 / period_s / 1e12 if valu_insts else None,
+                "achieved": valu_frame * 64 / period_s / 1e12 if valu_frame else None,
                 "peak": VALU_PEAK_TOPS,
                 "unit": "TOP/s",
-                "frac": valu_insts * 64 / period_s / 1e12 / VALU_PEAK_TOPS if valu_insts else None,
-                "achieved_per_launch": valu_insts * 64 / kernel_s / 1e12 if valu_insts else None,
+                "frac": valu_frame * 64 / period_s / 1e12 / VALU_PEAK_TOPS if valu_frame else None,
+                "achieved_per_launch": valu_frame * launch_frames * 64 / kernel_s / 1e12 if valu_frame else None,
                 "brute_force_equiv": brute_tops,
-                "brute_force_ops_per_launch": f_alg / steps / max(1, world),
+                "brute_force_ops_per_launch": f_alg / steps / max(1, world) * launch_frames,
                 "note": "achieved = issued VALU lane-ops per frame (profiles/pmc_traffic.json SQ_INSTS_VALU x 64) / "
                         "frame period; achieved_per_launch uses the launch duration instead; brute_force_equiv = "
                         "24 ops per sphere test + 17 per plane test over every primitive (SURVEY.md 8d) / kernel "
                         "time -- above peak where culling skips tests",
             },
             "cpu_baseline": None,
+            # host time spent issuing the timed steps, per step (includes the host's waits inside
+            # the loop, e.g. the N>1 pipeline's size handshake): ~ms_per_step when host-bound
+            "host_ms_per_step": host_s * 1e3,
         }
         if tg is not None:
             # wire bytes each rank shipped per frame (max over ranks, as gathered), vs the raw band set
             out["config"]["gather_wire_bytes_per_frame"] = tg.bytes_sent / steps
             out["config"]["gather_rgb24_bytes_per_frame"] = 3 * rb.slot_elems
-        if world == 1:
+        if world == 1 and not args.no_tick:
             # Tick() path for context: full frame into pinned host memory (PCIe D2H included); not `value`
             import numpy as np
             host = np.empty(W * H, dtype=np.int32)

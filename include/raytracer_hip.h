@@ -204,6 +204,13 @@ int rt_scatter_bands(rt_ctx* ctx, int width, int height, int band_rows, int band
 enum { RT_BANDS_INT32 = 0, RT_BANDS_RGB24 = 1, RT_BANDS_FRAME = 2 };
 int rt_render_bands_ex(rt_ctx* ctx, int width, int height, int band_rows, int band_first,
                        int band_step, void* d_out, int format, void* hip_stream, int* out_n_bands);
+/* n_frames frames of this rank's bands (the current camera, every frame traced in full) in
+ * ONE launch: frame f's output at d_out + f * frame_stride_bytes, in `format`.  For the
+ * multi-GPU pipeline, where a rank's share of a 1080p frame is a few microseconds of GPU work
+ * and one launch per frame would leave the GPU waiting for the host. */
+int rt_render_bands_batch(rt_ctx* ctx, int width, int height, int band_rows, int band_first,
+                          int band_step, int n_frames, void* d_out, size_t frame_stride_bytes,
+                          int format, void* hip_stream, int* out_n_bands);
 /* Reassemble the band sets of `world` ranks (band b rendered by rank b % world with
  * band_first = rank, band_step = world), gathered rank after rank at slot_bytes intervals
  * in d_gathered, into the row-major frame d_frame[height][width] -- one launch for all

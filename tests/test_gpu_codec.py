@@ -119,3 +119,36 @@ def test_encode_rejects_bad_arguments(gpu_ctx):
         gpu_ctx.encode_bands(64, 64, 8, 0, 1, buf.data_ptr(), 64, 1, wire.data_ptr())
     with pytest.raises(RayTracerError):  # misaligned wire
         gpu_ctx.encode_bands(64, 64, 8, 0, 1, buf.data_ptr(), 64 * 64, 1, wire.data_ptr() + 4)
+
+
+@pytest.mark.parametrize("fmt_name,world,rank", [("RT_BANDS_FRAME", 1, 0), ("RT_BANDS_FRAME", 3, 0), ("RT_BANDS_INT32", 2, 1),
+                                                 ("RT_BANDS_RGB24", 3, 2)])
+def test_batched_band_launch_equals_single_frames(gpu_ctx, fmt_name, world, rank):
+    """rt_render_bands_batch: n frames in one launch (grid z), each bit-identical to the
+    single-frame launch and written at its own stride; ray counters scale with n."""
+    import torch
+    from raytracer_hip import abi
+    fmt = getattr(abi, fmt_name)
+    sc = scenes.config("C3").resized(200, 120)
+    W, H, br, n = sc.width, sc.height, 8, 3
+    gpu_ctx.set_scene(sc)
+    rb = RowBands(W, H, br, rank, world)
+    per = W * H * 4 if fmt == abi.RT_BANDS_FRAME else rb.slot_elems * (3 if fmt == abi.RT_BANDS_RGB24 else 4)
+    stride = (per + 255) // 256 * 256 + 256
+    one = torch.full((stride,), 0x5A, dtype=torch.uint8, device="cuda")
+    many = torch.full((n * stride,), 0x5A, dtype=torch.uint8, device="cuda")
+    s = torch.cuda.current_stream().cuda_stream
+    gpu_ctx.reset_stats()
+    gpu_ctx.render_bands_ex(W, H, br, rank, world, one.data_ptr(), fmt, s)
+    torch.cuda.synchronize()
+    st1 = gpu_ctx.stats()
+    gpu_ctx.reset_stats()
+    gpu_ctx.render_bands_batch(W, H, br, rank, world, n, many.data_ptr(), stride, fmt, s)
+    torch.cuda.synchronize()
+    stn = gpu_ctx.stats()
+    want = one.cpu().numpy()
+    got = many.cpu().numpy().reshape(n, stride)
+    for f in range(n):
+        assert np.array_equal(got[f], want), f"frame {f} differs"
+    for k in ("primary_rays", "reflect_rays", "shadow_rays"):
+        assert stn[k] == n * st1[k], k

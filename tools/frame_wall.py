@@ -20,6 +20,8 @@ def main():
     ap.add_argument("--size", default="", help="WxH override")
     ap.add_argument("--inflight", type=int, default=1, help="frames in flight (streams/buffers)")
     ap.add_argument("--lib", default="", help="library build to load instead of the in-tree one")
+    ap.add_argument("--bands", default="", help="R/N: trace only rank R's 8-row bands of an N-rank world")
+    ap.add_argument("--batch", type=int, default=1, help="frames per launch (rt_render_bands_batch)")
     a = ap.parse_args()
     import torch
     from raytracer_hip import Context, abi, scenes
@@ -36,20 +38,39 @@ def main():
     ctx.set_scene(sc)
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(a.inflight - 1)]
     sp = [s.cuda_stream for s in streams]
+    ptrs = [o.data_ptr() for o in outs]
+    if a.batch > 1:
+        R, N = map(int, (a.bands or "0/1").split("/"))
+        big = [torch.empty(a.batch * W * H, dtype=torch.int32, device="cuda") for _ in range(a.inflight)]
+        bptr = [b.data_ptr() for b in big]
+        a.frames = a.frames // a.batch * a.batch
+
+        def frame(k):  # one launch per a.batch frames
+            if k % a.batch == 0:
+                i = (k // a.batch) % a.inflight
+                ctx.render_bands_batch(W, H, 8, R, N, a.batch, bptr[i], W * H * 4, abi.RT_BANDS_FRAME, sp[i])
+    elif a.bands:
+        R, N = map(int, a.bands.split("/"))
+
+        def frame(k):
+            ctx.render_bands_ex(W, H, 8, R, N, ptrs[k % a.inflight], abi.RT_BANDS_INT32, sp[k % a.inflight])
+    else:
+        def frame(k):
+            ctx.render_device(W, H, ptrs[k % a.inflight], sp[k % a.inflight])
     for k in range(20):
-        ctx.render_device(W, H, outs[k % a.inflight].data_ptr(), sp[k % a.inflight])
+        frame(k)
     torch.cuda.synchronize()
     res, enq = [], []
     for _ in range(a.reps):
         t0 = time.perf_counter()
         for k in range(a.frames):
-            ctx.render_device(W, H, outs[k % a.inflight].data_ptr(), sp[k % a.inflight])
+            frame(k)
         enq.append((time.perf_counter() - t0) / a.frames * 1e6)
         torch.cuda.synchronize()
         res.append((time.perf_counter() - t0) / a.frames * 1e6)
     st = ctx.stats()
     kern = st["kernel_ms"] / st["launches"] * 1e3 if st["kernel_ms"] else float("nan")
-    print(f"{os.path.basename(a.lib) or 'in-tree'} {a.config} {W}x{H} strip={a.strip or '-'} inflight={a.inflight}: "
+    print(f"{os.path.basename(a.lib) or 'in-tree'} {a.config} {W}x{H} strip={a.strip or '-'} bands={a.bands or '-'} batch={a.batch} inflight={a.inflight}: "
           f"wall/frame min {min(res):.2f} us median {sorted(res)[len(res)//2]:.2f} us; host enqueue/frame {min(enq):.2f} us")
 
 

@@ -3,7 +3,8 @@ counter for one kernel.  HBM traffic per launch follows MI355X_MICROARCH.md 'HBM
 FETCH_SIZE/WRITE_SIZE are in KiB; on gfx950 FETCH_SIZE reads 1/2 of the bytes of wide
 coalesced reads, so it is doubled; WRITE_SIZE is taken as is.
 
-    python tools/pmc_summary.py gpurun_out/pmc_C2 [kernel-substring] [--json out.json --config C2 --world 1]
+    python tools/pmc_summary.py gpurun_out/pmc_C2 [kernel-substring] [--json out.json --config C2 --world 1
+                                                                      --frames-per-launch 16]
 """
 import csv
 import glob
@@ -44,8 +45,9 @@ def main():
             data = json.load(open(out))
         except (OSError, ValueError):
             data = {}
+        fpl = int(sys.argv[sys.argv.index("--frames-per-launch") + 1]) if "--frames-per-launch" in sys.argv else 1
         data.setdefault(cfg, {})[world] = {
-            "hbm_bytes_per_launch": fetch + write, "fetch_size_kib": s.get("FETCH_SIZE"),
+            "hbm_bytes_per_launch": fetch + write, "frames_per_launch": fpl, "fetch_size_kib": s.get("FETCH_SIZE"),
             "write_size_kib": s.get("WRITE_SIZE"), "counters": s,
             "method": "rocprofv3 --pmc, one pass per counter group; FETCH_SIZE x2 (gfx950), KiB -> bytes"}
         json.dump(data, open(out, "w"), indent=1, sort_keys=True)

@@ -361,7 +361,7 @@ int view_tables(rt_ctx* ctx, Device& d, LaunchParams& lp) {
 
 // Launch the trace of bands (first, step) of `band_rows` rows into `out` on device d.
 int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int band_rows, int first, int step,
-                int32_t* out, int* n_bands, int fmt = RT_BANDS_INT32) {
+                int32_t* out, int* n_bands, int fmt = RT_BANDS_INT32, int n_frames = 1, size_t frame_bytes = 0) {
     LaunchParams lp;
     std::memset(&lp, 0, sizeof lp);
     int rc = view_params(ctx, W, H, lp);
@@ -375,6 +375,8 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
     lp.local_rows = nb * band_rows;
     lp.out = out;
     lp.out_fmt = fmt;
+    lp.n_frames = n_frames;
+    lp.out_frame_bytes = frame_bytes;
     hipStream_t saved = d.stream;
     d.stream = stream;
     const bool timed = begin_timed(ctx, d, 0);
@@ -385,7 +387,7 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
     ctx->launches++;
     for (int k = 0; k < nb; ++k) {  // pixels of rows < H in the launched bands
         const long long y0 = (long long)(first + k * step) * band_rows;
-        ctx->prim_rays += (uint64_t)std::min<long long>(band_rows, (long long)H - y0) * (uint64_t)W;
+        ctx->prim_rays += (uint64_t)std::min<long long>(band_rows, (long long)H - y0) * (uint64_t)W * (uint64_t)n_frames;
     }
     return RT_OK;
 }
@@ -716,6 +718,29 @@ int rt_render_bands_ex(rt_ctx* ctx, int width, int height, int band_rows, int ba
     rc = trace_bands(ctx, d, s, width, height, band_rows, band_first, band_step, (int32_t*)d_out, &nb, format);
     if (out_n_bands) *out_n_bands = nb;
     if (rc == RT_OK) ctx->pixels += (uint64_t)nb * band_rows * width;
+    return rc;
+}
+
+int rt_render_bands_batch(rt_ctx* ctx, int width, int height, int band_rows, int band_first, int band_step,
+                          int n_frames, void* d_out, size_t frame_stride_bytes, int format, void* hip_stream,
+                          int* out_n_bands) {
+    int rc = check_ctx(ctx, width, height);
+    if (rc != RT_OK) return rc;
+    if (band_rows <= 0 || band_first < 0 || band_step <= 0 || !d_out || n_frames <= 0 || n_frames > 65535 ||
+        (format != RT_BANDS_INT32 && format != RT_BANDS_RGB24 && format != RT_BANDS_FRAME))
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_bands_batch: bad band arguments");
+    if (ctx->n_gpus != 1) return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_bands_batch needs a single-GPU context");
+    const int nb = bands_of(height, band_rows, band_first, band_step);
+    const size_t need = format == RT_BANDS_FRAME ? (size_t)width * height * 4
+                                                 : (size_t)nb * band_rows * width * (format == RT_BANDS_RGB24 ? 3 : 4);
+    if (n_frames > 1 && frame_stride_bytes < need)
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_bands_batch: frame stride smaller than a frame's output");
+    Device& d = ctx->dev[0];
+    DeviceGuard guard(d.id);
+    rc = trace_bands(ctx, d, (hipStream_t)hip_stream, width, height, band_rows, band_first, band_step, (int32_t*)d_out,
+                     nullptr, format, n_frames, frame_stride_bytes);
+    if (out_n_bands) *out_n_bands = nb;
+    if (rc == RT_OK) ctx->pixels += (uint64_t)nb * band_rows * width * (uint64_t)n_frames;
     return rc;
 }
 

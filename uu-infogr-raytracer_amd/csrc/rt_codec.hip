@@ -294,21 +294,38 @@ __global__ __launch_bounds__(256) void encode_copy_kernel(const uint64_t* __rest
 // needs only the lane above (DPP row shift by one).  A wave decodes one chunk.
 constexpr int DEC_TPW = CODEC_TPW;
 
-__device__ __forceinline__ void decode_group(const unsigned char* __restrict__ gathered, size_t rank_stride,
-                                             int32_t* __restrict__ frames, const CodecGeom& g, int groups, size_t gw,
-                                             int lane) {
+// A group's header words, loaded one group ahead of its decode: the header load of group i+1
+// overlaps the payload loads and arithmetic of group i.
+struct DecHead {
+    const unsigned char* wire;
+    int rank, t0;
+    uint2 hdr;      // this lane's tile: first pixel, meta
+    uint32_t base;  // the chunk's unit offset
+};
+__device__ __forceinline__ DecHead decode_head(const unsigned char* __restrict__ gathered, size_t rank_stride,
+                                               const CodecGeom& g, int groups, size_t gw, int lane) {
+    DecHead h;
     const int rel_rank = (int)(gw / (size_t)groups);
-    const int t0 = (int)(gw - (size_t)rel_rank * groups) * DEC_TPW;
-    const int rank = g.rank + rel_rank;
-    const unsigned char* wire = gathered + (size_t)rank * rank_stride;
+    h.t0 = (int)(gw - (size_t)rel_rank * groups) * DEC_TPW;
+    h.rank = g.rank + rel_rank;
+    h.wire = gathered + (size_t)h.rank * rank_stride;
+    const int t = h.t0 + (lane >> 3);
+    h.hdr = ((const uint2*)wire_tile_hdr(h.wire))[t < g.n_tiles ? t : 0];
+    h.base = wire_chunk_base(h.wire, g)[h.t0 / CODEC_TPW];  // the wave's chunk
+    return h;
+}
+
+__device__ __forceinline__ void decode_group(int32_t* __restrict__ frames, const CodecGeom& g, const DecHead& h,
+                                             int lane) {
+    const int rank = h.rank, t0 = h.t0;
+    const unsigned char* wire = h.wire;
     const int total_bands = (g.H + g.band_rows - 1) / g.band_rows;
     const int nb = rank < total_bands ? (total_bands - 1 - rank) / g.world + 1 : 0;
     const int j = lane >> 3, ry = lane & 7;
     const int t = t0 + j;
     const bool live = t < g.n_tiles;
-    const uint2 hdr = ((const uint2*)wire_tile_hdr(wire))[live ? t : 0];
-    const uint32_t first = live ? hdr.x : 0u, meta = live ? hdr.y : 0u;
-    const uint32_t base = wire_chunk_base(wire, g)[t0 / CODEC_TPW];  // the wave's chunk
+    const uint32_t first = live ? h.hdr.x : 0u, meta = live ? h.hdr.y : 0u;
+    const uint32_t base = h.base;
     const TilePos tp = tile_pos(g, t0, j);
     const int f = tp.f, tr = tp.tr, tc = tp.tc;
     const int r = tr * 8 + ry;
@@ -369,8 +386,19 @@ __global__ __launch_bounds__(256) void decode_tiles_kernel(const unsigned char* 
     const int lane = threadIdx.x & 63;
     const int groups = (g.n_tiles + DEC_TPW - 1) / DEC_TPW;  // per rank
     const size_t n = (size_t)(g.world - g.rank) * (size_t)groups;  // ranks g.rank .. world-1
-    for (size_t gw = (size_t)blockIdx.x * 4 + wave_index(); gw < n; gw += (size_t)gridDim.x * 4)
-        decode_group(gathered, rank_stride, frames, g, groups, gw, lane);
+    const size_t stride = (size_t)gridDim.x * 4;
+    size_t gw = (size_t)blockIdx.x * 4 + wave_index();
+    if (gw >= n) return;  // wave-uniform
+    DecHead h = decode_head(gathered, rank_stride, g, groups, gw, lane);
+    for (;;) {
+        const size_t nx = gw + stride;
+        DecHead hn = h;
+        if (nx < n) hn = decode_head(gathered, rank_stride, g, groups, nx, lane);  // prefetch
+        decode_group(frames, g, h, lane);
+        if (nx >= n) break;
+        gw = nx;
+        h = hn;
+    }
 }
 
 int launch_encode_bands(const int32_t* bands, unsigned char* wire, const CodecGeom& g, int64_t* wire_bytes,

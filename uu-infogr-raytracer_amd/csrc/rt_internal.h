@@ -114,7 +114,9 @@ struct LaunchParams {
     // row mapping: local row r -> band (band_first + (r / band_rows) * band_step),
     // global row = band * band_rows + r % band_rows; pixel written at out[r * W + x].
     int band_rows, band_first, band_step, local_rows;
+    int n_frames;  // grid z (frames of one batch launch, all with this view); 0 = 1
     int32_t* out;
+    unsigned long long out_frame_bytes;  // batch launches: frame z of the grid at (char*)out + z * out_frame_bytes
     int out_fmt;  // 0: int32 0x00RRGGBB per pixel; 1: packed 24-bit (bytes B, G, R); 2: int32 at frame row y
     unsigned long long* counters;  // COUNTER_SLOTS x {primary, reflect, shadow, pad}
     int prim_const;                // 1: pc[0..S) and pbox[0..S) valid (S <= MAX_PRIM_CONST)

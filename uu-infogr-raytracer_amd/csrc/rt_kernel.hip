@@ -229,10 +229,11 @@ __device__ __forceinline__ uint32_t shift_channel(float c) {
 // Format 2 (RT_BANDS_FRAME): the rank's bands straight into the row-major frame (row y).
 __device__ __forceinline__ void store_pixel(const LaunchParams& p, int r, int y, int x, uint32_t px32) {
     const size_t i = (size_t)(p.out_fmt == 2 ? y : r) * (size_t)p.W + (size_t)x;
+    unsigned char* base = (unsigned char*)p.out + (size_t)blockIdx.z * p.out_frame_bytes;  // batch frame z
     if (p.out_fmt != 1) {
-        p.out[i] = (int32_t)px32;
+        ((int32_t*)base)[i] = (int32_t)px32;
     } else {
-        unsigned char* o = (unsigned char*)p.out + i * 3;
+        unsigned char* o = base + i * 3;
         o[0] = (unsigned char)px32;
         o[1] = (unsigned char)(px32 >> 8);
         o[2] = (unsigned char)(px32 >> 16);
@@ -1553,7 +1554,8 @@ RT_DEFINE_DISPATCH(launch_bundle, trace_bundle_kernel)
 
 int launch_trace(const LaunchParams& p, bool generic_pow, void* stream) {
     if (p.local_rows <= 0 || p.W <= 0) return (int)hipSuccess;
-    const dim3 grid((unsigned)((p.W + TILE_W - 1) / TILE_W), (unsigned)((p.local_rows + TILE_H - 1) / TILE_H));
+    const dim3 grid((unsigned)((p.W + TILE_W - 1) / TILE_W), (unsigned)((p.local_rows + TILE_H - 1) / TILE_H),
+                    (unsigned)(p.n_frames > 1 ? p.n_frames : 1));
     const dim3 block(WG_THREADS);
     hipStream_t s = (hipStream_t)stream;
     // bundle culling pays for its per-wave bounds only with enough spheres (A/B: +15 % at

@@ -148,6 +148,16 @@ class Context:
                                                 C.c_void_p(d_ptr), fmt, C.c_void_p(stream), C.byref(nb)))
         return nb.value
 
+    def render_bands_batch(self, width: int, height: int, band_rows: int, band_first: int, band_step: int,
+                           n_frames: int, d_ptr: int, frame_stride_bytes: int, fmt: int = abi.RT_BANDS_INT32,
+                           stream: int = 0) -> int:
+        """n_frames frames of these bands in one launch (rt_render_bands_batch)."""
+        nb = C.c_int(0)
+        self._check(self.lib.rt_render_bands_batch(self.ptr, width, height, band_rows, band_first, band_step, n_frames,
+                                                   C.c_void_p(d_ptr), frame_stride_bytes, fmt, C.c_void_p(stream),
+                                                   C.byref(nb)))
+        return nb.value
+
     def scatter_gathered(self, width: int, height: int, band_rows: int, world: int, d_gathered: int,
                          rank_stride: int, d_frame: int, fmt: int = abi.RT_BANDS_RGB24, stream: int = 0):
         """Reassemble all ranks' band sets (rank r's at d_gathered + r * rank_stride) into d_frame."""

@@ -111,6 +111,8 @@ EXPORTS = [
                                    C.c_void_p, C.c_void_p]),
     ("rt_render_bands_ex", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int,
                                      C.c_void_p, C.POINTER(C.c_int)]),
+    ("rt_render_bands_batch", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                        C.c_size_t, C.c_int, C.c_void_p, C.POINTER(C.c_int)]),
     ("rt_scatter_gathered", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_size_t,
                                       C.c_int, C.c_void_p, C.c_void_p]),
     ("rt_wire_layout_of", C.c_int, [C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(rt_wire_layout)]),

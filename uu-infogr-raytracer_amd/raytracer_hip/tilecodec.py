@@ -10,18 +10,18 @@ band sets before the gather and rank 0 decodes them straight into the frame:
   Every rank uses the tile grid of the largest band set (`max_bands` bands), so the fixed
   part of the wire has the same size on every rank.  A batch of F frames is F tile grids
   one after the other.
-* Pixel (rx, ry) of a tile (lane ry*8 + rx) is predicted by its left neighbour; the first
-  column by the pixel above in odd rows and by the tile's first pixel in even rows (the
-  predictors a DPP row shift inside 16 lanes, or a scalar, delivers on the GPU); pixel
-  (0, 0) is stored raw in the tile header.  Residuals
+* Pixel (rx, ry) of a tile is predicted by its left neighbour; the first column by the pixel
+  above in odd rows and by the tile's first pixel in even rows (on the GPU a lane holds one
+  tile row: the left prediction runs in registers, the row above is one DPP row shift, the
+  first pixel one broadcast); pixel (0, 0) is stored raw in the tile header.  Residuals
   are per channel, modulo 256, zigzag-mapped to 0..255 (0, -1, 1, -2, ... -> 0, 1, 2, 3).
   Pixels outside the frame (columns >= width, rows of missing bands or past the height)
   have residual 0 and are never written by the decoder.
 * Channel c (R, G, B) of a tile gets a width w_c in {0, 1, 2, 4, 8}: the bit length of its
   largest zigzag residual rounded up to a power of two.  Its segment is w_c 8-byte units =
   64 * w_c bits, lane l's residual at bits [l*w_c, (l+1)*w_c) of the little-endian stream
-  (inside one 32-bit word, since w_c divides 32): the GPU packs a word with a DPP OR over
-  32 / w_c lanes and unpacks a lane with one load, a shift and a mask.
+  (inside one 32-bit word, since w_c divides 32): a tile row's residuals of a channel are
+  w_c consecutive bytes, one store / load per GPU lane.
 * Tiles are grouped in chunks of 8 consecutive tiles (one wave's tiles on the GPU); a
   tile's payload offset is its chunk's base (a 32-bit unit offset, one per chunk) plus its
   offset inside the chunk (kept in the header).  Segments follow each other R, G, B.
