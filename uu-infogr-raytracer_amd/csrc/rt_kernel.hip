@@ -749,16 +749,52 @@ __device__ __forceinline__ f3 shade_direct(const LaunchParams& p, bool is_sphere
 #ifndef RT_PRIM_BOX
 #define RT_PRIM_BOX 1
 #endif
+// RT_FAST_PROLOGUE (shipped): the wave's start has no dependent chain of memory round trips --
+// the box is one unconditional 16-byte load (lane 0's for lanes >= S), tested without
+// short-circuit branches, and the view-table loads are issued before it (tile_prologue).
+#ifndef RT_FAST_PROLOGUE
+#define RT_FAST_PROLOGUE 1
+#endif
 __device__ __forceinline__ unsigned long long prim_box_mask(const LaunchParams& p, int x, int y) {
     const int x_lo = __builtin_amdgcn_readlane(x, 0), x_hi = __builtin_amdgcn_readlane(x, 63);
     const int y_lo = __builtin_amdgcn_readlane(y, 0), y_hi = __builtin_amdgcn_readlane(y, 63);
     const int lane = threadIdx.x & 63;
     bool cand = false;
-    if (lane < p.S) {
+    if constexpr (RT_FAST_PROLOGUE) {
+        const bool in = lane < p.S;
+        const PrimBox b = p.pbox[in ? lane : 0];
+        cand = in & (b.x0 <= x_hi) & (b.x1 >= x_lo) & (b.y0 <= y_hi) & (b.y1 >= y_lo);
+    } else if (lane < p.S) {
         const PrimBox b = p.pbox[lane];
         cand = b.x0 <= x_hi && b.x1 >= x_lo && b.y0 <= y_hi && b.y1 >= y_lo;
     }
     return __builtin_amdgcn_ballot_w64(cand);
+}
+
+// A wave's pixels: column x, local row r -> frame row y (band band_first + (r / band_rows) *
+// band_step), validity, and the view-table entries lx = lxt[x], ly = lyt[y] (0 outside).
+// Fast paths without a per-lane integer division: one band (every full-frame launch) and the
+// 8-row bands of the multi-GPU path.
+struct TilePixel {
+    int x, r, y;
+    bool valid;
+    float lx, ly;
+};
+__device__ __forceinline__ TilePixel tile_pixel(const LaunchParams& p, int x, int r) {
+    TilePixel t;
+    t.x = x, t.r = r;
+    if (RT_FAST_PROLOGUE && p.band_rows >= p.local_rows) {  // wave-uniform branches
+        t.y = p.band_first * p.band_rows + r;
+    } else if (RT_FAST_PROLOGUE && p.band_rows == 8) {
+        t.y = (p.band_first + (r >> 3) * p.band_step) * 8 + (r & 7);
+    } else {
+        const int band = p.band_first + (r / p.band_rows) * p.band_step;
+        t.y = band * p.band_rows + (r % p.band_rows);
+    }
+    t.valid = x < p.W && r < p.local_rows && t.y < p.H;
+    const float lx = p.lxt[t.valid ? x : 0], ly = p.lyt[t.valid ? t.y : 0];  // unconditional loads
+    t.lx = t.valid ? lx : 0.0f, t.ly = t.valid ? ly : 0.0f;
+    return t;
 }
 
 template <bool PRIMARY, int SMAX>
@@ -859,11 +895,10 @@ __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p
     __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * WG_THREADS : 1];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int x = blockIdx.x * TILE_W + (wave % WG_WX) * 8 + (lane & 7);
-    const int r = blockIdx.y * TILE_H + (wave / WG_WX) * 8 + (lane >> 3);
-    const int band = p.band_first + (r / p.band_rows) * p.band_step;
-    const int y = band * p.band_rows + (r % p.band_rows);
-    const bool valid = x < p.W && r < p.local_rows && y < p.H;
+    const TilePixel tpx = tile_pixel(p, blockIdx.x * TILE_W + (wave % WG_WX) * 8 + (lane & 7),
+                                     blockIdx.y * TILE_H + (wave / WG_WX) * 8 + (lane >> 3));
+    const int x = tpx.x, r = tpx.r, y = tpx.y;
+    const bool valid = tpx.valid;
     const unsigned long long pmask = (RT_PRIM_BOX && p.prim_const) ? prim_box_mask(p, x, y) : 0;
 
     unsigned cnt = 0;  // packed: reflected segments (bits 0-7) | shadow rays << CNT_SHADOW_SHIFT
@@ -872,7 +907,7 @@ __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p
         // TracePixel primary ray, :963-971 (no half-pixel offset)
         // lx = ((float)x / W - 0.5f) * pw, ly likewise: per-column / per-row tables built on
         // the host with the same binary32 operations (view_tables in rt_api.cpp)
-        const float lx = p.lxt[x], ly = p.lyt[y], lz = 1.0f * p.nearc;
+        const float lx = tpx.lx, ly = tpx.ly, lz = 1.0f * p.nearc;
         const f3 vp = add(add(add(cam, scale(mk(p.right[0], p.right[1], p.right[2]), lx)),
                               scale(mk(p.up[0], p.up[1], p.up[2]), ly)),
                           scale(mk(p.fwd[0], p.fwd[1], p.fwd[2]), lz));
@@ -1319,17 +1354,16 @@ __global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel(LaunchParams p
     __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * WG_THREADS : 1];
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
-    const int x = blockIdx.x * TILE_W + (wave % WG_WX) * 8 + (lane & 7);
-    const int r = blockIdx.y * TILE_H + (wave / WG_WX) * 8 + (lane >> 3);
-    const int band = p.band_first + (r / p.band_rows) * p.band_step;
-    const int y = band * p.band_rows + (r % p.band_rows);
-    const bool valid = x < p.W && r < p.local_rows && y < p.H;
+    const TilePixel tpx = tile_pixel(p, blockIdx.x * TILE_W + (wave % WG_WX) * 8 + (lane & 7),
+                                     blockIdx.y * TILE_H + (wave / WG_WX) * 8 + (lane >> 3));
+    const int x = tpx.x, r = tpx.r, y = tpx.y;
+    const bool valid = tpx.valid;
 
     unsigned cnt = 0;  // packed: reflected segments (bits 0-7) | shadow rays << CNT_SHADOW_SHIFT
     const f3 cam = mk(p.cam[0], p.cam[1], p.cam[2]);
     // TracePixel primary ray, :963-971 (no half-pixel offset)
     // per-column / per-row tables (see the direct kernel); lanes outside the frame read 0
-    const float lx = valid ? p.lxt[x] : 0.0f, ly = valid ? p.lyt[y] : 0.0f, lz = 1.0f * p.nearc;
+    const float lx = tpx.lx, ly = tpx.ly, lz = 1.0f * p.nearc;
     const f3 vp = add(add(add(cam, scale(mk(p.right[0], p.right[1], p.right[2]), lx)),
                           scale(mk(p.up[0], p.up[1], p.up[2]), ly)),
                       scale(mk(p.fwd[0], p.fwd[1], p.fwd[2]), lz));
