@@ -175,3 +175,74 @@ def test_compose_empty_pool_draws_circles_only():
                     np.zeros(0, dtype=rh.SEGMENT_DTYPE))
     assert set(np.unique(out).tolist()) <= {0, dv.CIRCLE_COLOR}
     assert (out == dv.CIRCLE_COLOR).any()
+
+
+# -- Surface.Print (surface.cs:107-131) ---------------------------------------------------
+
+def _print_scalar(pixels, width, t, x, y, c):
+    """Statement-by-statement walk of surface.cs:121-130 over the atlas mask (C# IndexOutOfRange
+    becomes IndexError at the first store outside the array)."""
+    font = dv.font_mask().reshape(-1)
+    fw = dv.font_mask().shape[1]
+    fh = dv.font_mask().shape[0]
+    redir = [0] * 256
+    for i, ch in enumerate(dv.FONT_CHARS):
+        redir[ord(ch) & 255] = i
+    units = np.frombuffer(t.encode("utf-16-le"), dtype="<u2")
+    for i, unit in enumerate(units):
+        f = redir[int(unit) & 255]
+        dest = x + i * 12 + y * width
+        src = f * 12
+        for v in range(fh):
+            for u in range(12):
+                if font[src + u]:
+                    if not 0 <= dest + u < pixels.size:
+                        raise IndexError(dest + u)
+                    pixels[dest + u] = c
+            src += fw
+            dest += width
+
+
+def test_font_mask_matches_the_reference_atlas():
+    m = dv.font_mask()
+    assert m.shape == (16, 1082)
+    assert int(m.sum()) == 4676  # tools/make_font_mask.py over assets/font.png
+    assert len(dv.FONT_CHARS) == 90 and 90 * dv.FONT_GLYPH_W <= m.shape[1]
+    assert not m[:, 89 * 12:90 * 12].any()  # the space glyph is blank
+
+
+@pytest.mark.parametrize("text,x,y", [("Hello, World!", 3, 2), ("0123456789 {}[];:<>,.?/\\", 0, 20),
+                                      ("unknown: é€~|", 5, 40), ("", 0, 0),
+                                      ("wraps into the next row", 150, 5)])
+def test_print_matches_scalar_walk(text, x, y):
+    W, H = 200, 64
+    a = np.zeros(W * H, dtype=np.int32)
+    b = a.copy()
+    dv.surface_print(a, W, text, x, y, 0x123456)
+    _print_scalar(b, W, text, x, y, 0x123456)
+    np.testing.assert_array_equal(a, b)
+    assert (a != 0).any() == any(ch != " " for ch in text)
+
+
+def test_print_unknown_characters_use_glyph_zero():
+    W, H = 40, 20
+    a, b = np.zeros(W * H, dtype=np.int32), np.zeros(W * H, dtype=np.int32)
+    dv.surface_print(a, W, "~", 1, 1, 7)   # '~' is not in the glyph table
+    dv.surface_print(b, W, "A", 1, 1, 7)
+    np.testing.assert_array_equal(a, b)
+    s = rh.Surface(W, H)
+    s.Print("A", 1, 1, 7)
+    np.testing.assert_array_equal(s.pixels, b)
+
+
+def test_print_out_of_range_raises_after_earlier_stores():
+    W, H = 30, 20
+    a, b = np.zeros(W * H, dtype=np.int32), np.zeros(W * H, dtype=np.int32)
+    with pytest.raises(IndexError):
+        dv.surface_print(a, W, "AB", 2, 10, 9)     # glyph rows run past the last row
+    with pytest.raises(IndexError):
+        _print_scalar(b, W, "AB", 2, 10, 9)
+    np.testing.assert_array_equal(a, b)
+    assert (a == 9).any()
+    with pytest.raises(IndexError):
+        dv.surface_print(np.zeros(W * H, dtype=np.int32), W, "A", -40, 0, 9)  # negative index

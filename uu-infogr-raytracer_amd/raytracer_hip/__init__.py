@@ -18,7 +18,7 @@ import numpy as np
 
 from . import abi, debugview, scenes
 from .abi import RayTracerError, check, load_library
-from .debugview import SEGMENT_DTYPE, DebugView, surface_line
+from .debugview import SEGMENT_DTYPE, DebugView, surface_line, surface_print
 from .dist import bands_of
 
 __all__ = ["Surface", "RayTracer", "Context", "RayTracerError", "scenes", "abi", "load_library",
@@ -60,6 +60,9 @@ class Surface:
 
     def Line(self, x1: int, y1: int, x2: int, y2: int, c: int):  # surface.cs:57-100
         surface_line(self.pixels, self.width, self.height, x1, y1, x2, y2, c)
+
+    def Print(self, t: str, x: int, y: int, c: int):  # surface.cs:107-131
+        surface_print(self.pixels, self.width, t, x, y, c)
 
     def save_ppm(self, path: str):
         """Headless display hand-off (rt_write_ppm): the frame as a binary PPM."""
