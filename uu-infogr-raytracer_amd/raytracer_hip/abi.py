@@ -11,7 +11,8 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libraytracer_hip.so")
+# RAYTRACER_HIP_LIB selects another build of the library (A/B variants under lib/ab/)
+LIB_PATH = os.environ.get("RAYTRACER_HIP_LIB") or os.path.join(PKG_ROOT, "lib", "libraytracer_hip.so")
 
 RT_ABI_VERSION = 4  # include/raytracer_hip.h
 RT_BANDS_INT32, RT_BANDS_RGB24, RT_BANDS_FRAME = 0, 1, 2
