@@ -32,7 +32,10 @@
 namespace rtk {
 
 constexpr int CODEC_TPW = 8;     // tiles per wave = tiles per chunk
-constexpr int CODEC_BLOCKS = 2048;   // resident grid: 256 CUs x 8 workgroups of 4 waves
+#ifndef RT_ENC_BLOCKS
+#define RT_ENC_BLOCKS 2048
+#endif
+constexpr int CODEC_BLOCKS = RT_ENC_BLOCKS;  // encode grid: 256 CUs x 8 workgroups of 4 waves
 constexpr int CODEC_MAX_PER = 1024;  // chunks per workgroup at most (LDS of the copy pass)
 constexpr int STAGE_WORDS = 48;  // staging words per tile (3 channels x 8 bits x 64 lanes / 32)
 constexpr int STAGE_UNITS = STAGE_WORDS / 2;
@@ -118,19 +121,25 @@ __device__ __forceinline__ uint32_t width_of(uint32_t o) {
 // Encode one group of CODEC_TPW tiles (one chunk): tile headers with chunk-relative offsets,
 // the chunk total into chunk_base[chunk], the non-flat tiles' segments into their staging
 // slots (STAGE_WORDS per tile, final byte layout).  Returns the chunk total (units).
-__device__ __forceinline__ uint32_t encode_group(const int32_t* __restrict__ bands, unsigned char* __restrict__ wire,
-                                                 uint32_t* __restrict__ stage, const CodecGeom& g, int chunk, int lane) {
+// A lane's tile row of a chunk: its 8 pixels (0 outside the frame) and how many exist.
+struct EncRow {
+    uint32_t p[8];
+    int ncols;
+};
+__device__ __forceinline__ EncRow encode_load(const int32_t* __restrict__ bands, const CodecGeom& g, int chunk,
+                                              int lane) {
     const int t0 = chunk * CODEC_TPW;
     const int j = lane >> 3, ry = lane & 7;
-    const int t = t0 + j;
-    const bool live = t < g.n_tiles;
+    const bool live = t0 + j < g.n_tiles;
     const TilePos tp = tile_pos(g, t0, j);
     const int r = tp.tr * 8 + ry;
     const bool row_ok = live && r < g.n_bands * g.band_rows && frame_row(g, g.rank, r) < g.H;
     const int x0 = tp.tc * 8;
     const int ncols = row_ok ? min(8, g.W - x0) : 0;
     const int32_t* src = bands + (size_t)tp.f * g.frame_stride + (size_t)r * (size_t)g.W + (size_t)x0;
-    uint32_t p[8];
+    EncRow e;
+    e.ncols = ncols;
+    uint32_t* p = e.p;
     if (ncols == 8 && ((uintptr_t)src & 15) == 0) {
         const int4 a = ((const int4*)src)[0], b = ((const int4*)src)[1];
         p[0] = (uint32_t)a.x, p[1] = (uint32_t)a.y, p[2] = (uint32_t)a.z, p[3] = (uint32_t)a.w;
@@ -141,6 +150,17 @@ __device__ __forceinline__ uint32_t encode_group(const int32_t* __restrict__ ban
     }
 #pragma unroll
     for (int rx = 0; rx < 8; ++rx) p[rx] &= 0xffffffu;  // pixels outside the frame are 0
+    return e;
+}
+
+__device__ __forceinline__ uint32_t encode_group(unsigned char* __restrict__ wire, uint32_t* __restrict__ stage,
+                                                 const CodecGeom& g, int chunk, int lane, const EncRow& e) {
+    const int t0 = chunk * CODEC_TPW;
+    const int j = lane >> 3, ry = lane & 7;
+    const int t = t0 + j;
+    const bool live = t < g.n_tiles;
+    const int ncols = e.ncols;
+    const uint32_t* p = e.p;
     // residuals: left neighbour; first column: above (odd rows) or the tile's first pixel
     const uint32_t first = (uint32_t)__shfl((int)p[0], lane & ~7, 64);
     const uint32_t above = row_shr<1>(p[0]);
@@ -204,7 +224,8 @@ __global__ __launch_bounds__(256) void encode_tiles_kernel(const int32_t* __rest
     const int lane = threadIdx.x & 63, wave = wave_index();
     const int lo = blockIdx.x * per, hi = min(g.n_chunks, lo + per);
     uint32_t mine = 0;
-    for (int chunk = lo + wave; chunk < hi; chunk += 4) mine += encode_group(bands, wire, stage, g, chunk, lane);
+    for (int chunk = lo + wave; chunk < hi; chunk += 4)
+        mine += encode_group(wire, stage, g, chunk, lane, encode_load(bands, g, chunk, lane));
     if (lane == 0) s_tot[wave] = mine;
     __syncthreads();
     if (threadIdx.x == 0) wg_total[blockIdx.x] = s_tot[0] + s_tot[1] + s_tot[2] + s_tot[3];
@@ -293,6 +314,16 @@ __global__ __launch_bounds__(256) void encode_copy_kernel(const uint64_t* __rest
 // aligned 8-byte load), the prefix along the row runs in registers, and the first column
 // needs only the lane above (DPP row shift by one).  A wave decodes one chunk.
 constexpr int DEC_TPW = CODEC_TPW;
+// decode grid: 4096 workgroups of 4 waves (4 per SIMD; 2048 / 8192 / 16384: +7 / +2 / +14 %)
+#ifndef RT_DEC_BLOCKS
+#define RT_DEC_BLOCKS 4096
+#endif
+#ifndef RT_DEC_NT
+#define RT_DEC_NT 1
+#endif
+#ifndef RT_DEC_LDS
+#define RT_DEC_LDS 1
+#endif
 
 // A group's header words, loaded one group ahead of its decode: the header load of group i+1
 // overlaps the payload loads and arithmetic of group i.
@@ -365,6 +396,38 @@ __device__ __forceinline__ void decode_group(int32_t* __restrict__ frames, const
     px[0] = add_bytes(first, (ry & 1) ? add_bytes(d[0], d0_above) : d[0]) & 0xffffffu;
 #pragma unroll
     for (int rx = 1; rx < 8; ++rx) px[rx] = add_bytes(px[rx - 1], d[rx]) & 0xffffffu;
+    // A group of 8 tiles of one tile row, inside the width, on 16-byte aligned rows (wave-uniform;
+    // every group of a frame whose width is a multiple of 64): the wave's 8 rows x 64 pixels go
+    // through LDS so that each store instruction writes whole row segments (8 lanes x 16 B =
+    // 128 B of one row) instead of 16-byte pieces 32 bytes apart (RT_DEC_LDS).
+    if constexpr (RT_DEC_LDS) {
+        const int tc0 = __builtin_amdgcn_readfirstlane(tc);  // lane 0: j = 0
+        const bool full = t0 + DEC_TPW <= g.n_tiles && tc0 + DEC_TPW <= g.tiles_x && (tc0 + DEC_TPW) * 8 <= g.W &&
+                          (g.W & 3) == 0 && (g.frame_stride & 3) == 0 && ((uintptr_t)frames & 15) == 0;
+        if (full) {
+            __shared__ uint4 xch[4][8][16];  // [wave][row][16 B]
+            uint4(*rows)[16] = xch[wave_index()];
+            rows[ry][2 * j] = make_uint4(px[0], px[1], px[2], px[3]);
+            rows[ry][2 * j + 1] = make_uint4(px[4], px[5], px[6], px[7]);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint4 a = rows[ry][j], b = rows[ry][8 + j];
+            __builtin_amdgcn_wave_barrier();  // (the next group's writes come after these reads)
+            if (row_ok) {
+                uint4* dst = (uint4*)(frames + (size_t)f * g.frame_stride + (size_t)y * (size_t)g.W + (size_t)tc0 * 8);
+                if constexpr (RT_DEC_NT) {
+                    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+                    __builtin_nontemporal_store(u32x4{a.x, a.y, a.z, a.w}, (u32x4*)(dst + j));
+                    __builtin_nontemporal_store(u32x4{b.x, b.y, b.z, b.w}, (u32x4*)(dst + 8 + j));
+                } else {
+                    dst[j] = a;
+                    dst[8 + j] = b;
+                }
+            }
+            return;
+        }
+    }
     if (!row_ok) return;
     int32_t* dst = frames + (size_t)f * g.frame_stride + (size_t)y * (size_t)g.W + (size_t)x0;
     if (x0 + 8 <= g.W && ((uintptr_t)dst & 15) == 0) {
@@ -429,7 +492,7 @@ int launch_decode_gathered(const unsigned char* gathered, size_t rank_stride, in
                            void* stream) {
     const size_t waves = (size_t)(g.world - g.rank) * (size_t)((g.n_tiles + DEC_TPW - 1) / DEC_TPW);
     if (waves == 0) return (int)hipSuccess;
-    hipLaunchKernelGGL(decode_tiles_kernel, dim3((unsigned)std::min<size_t>((waves + 3) / 4, CODEC_BLOCKS)), dim3(256), 0,
+    hipLaunchKernelGGL(decode_tiles_kernel, dim3((unsigned)std::min<size_t>((waves + 3) / 4, RT_DEC_BLOCKS)), dim3(256), 0,
                        (hipStream_t)stream,
                        gathered, rank_stride, frames, g);
     return (int)hipGetLastError();
