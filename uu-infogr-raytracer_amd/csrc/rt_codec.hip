@@ -81,6 +81,40 @@ __device__ __forceinline__ uint32_t row_shr(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 + N, 0xf, 0xf, true);
 }
 
+// RT_ENC_DPP: the encoder's cross-lane steps without LDS round trips (ds_bpermute): the tile's
+// first pixel by a quad broadcast + a 4-lane shift into the upper quad, the tile OR as an
+// all-lanes butterfly (quad xor 1, quad xor 2, half-row mirror), the chunk-relative offsets
+// as a DPP wave scan (row shifts + row broadcasts) of the group totals.
+#ifndef RT_ENC_DPP
+#define RT_ENC_DPP 1
+#endif
+template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf, bool BOUND = true>
+__device__ __forceinline__ uint32_t dpp(uint32_t old, uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROW_MASK, BANK_MASK, BOUND);
+}
+// lane 8j's value in every lane of its 8-lane group
+__device__ __forceinline__ uint32_t group8_first(uint32_t v) {
+    const uint32_t q = dpp<0x00>(0u, v);            // quad_perm [0,0,0,0]
+    return dpp<0x114, 0xf, 0xa, false>(q, q);        // row_shr:4 into lanes 4-7, 12-15 of each row
+}
+// OR of the 8 lanes of each group, in every lane
+__device__ __forceinline__ uint32_t group8_or(uint32_t v) {
+    v |= dpp<0xb1>(0u, v);   // quad_perm [1,0,3,2]
+    v |= dpp<0x4e>(0u, v);   // quad_perm [2,3,0,1]
+    v |= dpp<0x141>(0u, v);  // row_half_mirror
+    return v;
+}
+// inclusive scan over the wave (all 64 lanes active)
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
+    x += row_shr<1>(x);
+    x += row_shr<2>(x);
+    x += row_shr<4>(x);
+    x += row_shr<8>(x);
+    x += dpp<0x142, 0xa, 0xf, false>(0u, x);  // row_bcast:15 -> rows 1, 3
+    x += dpp<0x143, 0xc, 0xf, false>(0u, x);  // row_bcast:31 -> rows 2, 3
+    return x;
+}
+
 __device__ __forceinline__ uint32_t bitlen8(uint32_t v) { return v ? 32u - (uint32_t)__builtin_clz(v) : 0u; }
 __device__ __forceinline__ uint32_t units_of(uint32_t wm) { return (wm & 15u) + ((wm >> 4) & 15u) + ((wm >> 8) & 15u); }
 
@@ -162,7 +196,7 @@ __device__ __forceinline__ uint32_t encode_group(unsigned char* __restrict__ wir
     const int ncols = e.ncols;
     const uint32_t* p = e.p;
     // residuals: left neighbour; first column: above (odd rows) or the tile's first pixel
-    const uint32_t first = (uint32_t)__shfl((int)p[0], lane & ~7, 64);
+    const uint32_t first = RT_ENC_DPP ? group8_first(p[0]) : (uint32_t)__shfl((int)p[0], lane & ~7, 64);
     const uint32_t above = row_shr<1>(p[0]);
     uint32_t z[8];
     z[0] = ncols > 0 ? zigzag_bytes(sub_bytes(p[0], (ry & 1) ? above : first)) & 0xffffffu : 0u;
@@ -170,21 +204,33 @@ __device__ __forceinline__ uint32_t encode_group(unsigned char* __restrict__ wir
     for (int rx = 1; rx < 8; ++rx) z[rx] = rx < ncols ? zigzag_bytes(sub_bytes(p[rx], p[rx - 1])) & 0xffffffu : 0u;
     // tile OR of residuals -> widths (lane 8j+7 accumulates lanes 8j..8j+7), broadcast
     uint32_t o = z[0] | z[1] | z[2] | z[3] | z[4] | z[5] | z[6] | z[7];
-    o |= row_shr<1>(o);
-    o |= row_shr<2>(o);
-    o |= row_shr<4>(o);
-    uint32_t wm = width_of((o >> 16) & 0xffu) | (width_of((o >> 8) & 0xffu) << 4) | (width_of(o & 0xffu) << 8);
-    wm = (uint32_t)__shfl((int)wm, lane | 7, 64);
-    if (!live) wm = 0;
-    const uint32_t u = units_of(wm);
-    // chunk-relative offsets: inclusive scan over the group leaders (lanes 8j+7)
-    uint32_t incl = ry == 7 ? u : 0u;
+    uint32_t wm, incl, rel;
+    if constexpr (RT_ENC_DPP) {
+        o = group8_or(o);
+        wm = width_of((o >> 16) & 0xffu) | (width_of((o >> 8) & 0xffu) << 4) | (width_of(o & 0xffu) << 8);
+        if (!live) wm = 0;
+        // chunk-relative offsets: with each group's units in its lane 8j+7 only, the inclusive
+        // scan at lanes 8j..8j+6 is already the sum over the groups before j
+        const uint32_t u7 = ry == 7 ? units_of(wm) : 0u;
+        incl = wave_scan_incl(u7);
+        rel = incl - u7;
+    } else {
+        o |= row_shr<1>(o);
+        o |= row_shr<2>(o);
+        o |= row_shr<4>(o);
+        wm = width_of((o >> 16) & 0xffu) | (width_of((o >> 8) & 0xffu) << 4) | (width_of(o & 0xffu) << 8);
+        wm = (uint32_t)__shfl((int)wm, lane | 7, 64);
+        if (!live) wm = 0;
+        const uint32_t u = units_of(wm);
+        // chunk-relative offsets: inclusive scan over the group leaders (lanes 8j+7)
+        incl = ry == 7 ? u : 0u;
 #pragma unroll
-    for (int k = 8; k < 64; k <<= 1) {
-        const uint32_t x = (uint32_t)__shfl_up((int)incl, k, 64);
-        if (lane >= k) incl += x;
+        for (int k = 8; k < 64; k <<= 1) {
+            const uint32_t x = (uint32_t)__shfl_up((int)incl, k, 64);
+            if (lane >= k) incl += x;
+        }
+        rel = (uint32_t)__shfl((int)(incl - u), lane | 7, 64);
     }
-    const uint32_t rel = (uint32_t)__shfl((int)(incl - u), lane | 7, 64);
     if (live && ry == 0) ((uint2*)wire_tile_hdr(wire))[t] = make_uint2(first, wm | (rel << 12));
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     if (lane == 63) wire_chunk_base(wire, g)[chunk] = total;  // chunk total, scanned later
