@@ -38,6 +38,8 @@ def parse():
     ap.add_argument("--warmup", type=int, default=200,
                     help="untimed frames first: the GPU needs ~10 ms of load to reach steady clocks")
     ap.add_argument("--config", default="C2")
+    ap.add_argument("--size", default="",
+                    help="WxH: probe runs only -- the config's scene at another frame size (never the bench line)")
     ap.add_argument("--band-rows", type=int, default=8)
     ap.add_argument("--frames-per-launch", type=int, default=16,
                     help="N=1: frames traced per launch (rt_render_bands_batch; every frame in full, the same "
@@ -47,8 +49,12 @@ def parse():
                          "slot; every frame is fully traced)")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="N>1: gather each frame before tracing the next (no double buffering)")
-    ap.add_argument("--batch", type=int, default=16,
-                    help="N>1: frames per RCCL gather (pipelined; 1 = one gather per frame)")
+    ap.add_argument("--batch", type=int, default=0,
+                    help="N>1: frames per RCCL gather (pipelined; 1 = one gather per frame).  0 = auto: 64, "
+                         "fewer for short runs (steps // 4, at least 8).  A batch boundary costs the host "
+                         "~100-200 us (codec calls, two collectives, a size read-back): at 16 frames per "
+                         "gather that, not the GPU, bounded a rank's 1/8 share of 1080p (8.9 vs 3.0 us per "
+                         "frame, tools/overhead_probe.sh)")
     ap.add_argument("--band-format", choices=["tiles", "rgb24", "int32"], default="tiles",
                     help="N>1: band sets shipped to rank 0 tile-encoded (lossless, rt_encode_bands), as packed "
                          "24-bit RGB or as int32 pixels")
@@ -116,6 +122,8 @@ def load_pmc(path, config, world):
 
 def main():
     args = parse()
+    if args.batch <= 0:
+        args.batch = 64 if args.steps >= 256 else max(8, args.steps // 4)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -135,6 +143,9 @@ def main():
     else:
         torch.cuda.set_device(0)
     sc = scenes.config(args.config)
+    if args.size:
+        w_, h_ = map(int, args.size.lower().split("x"))
+        sc = sc.resized(w_, h_, f"{sc.name}@{w_}x{h_}")
     W, H = sc.width, sc.height
     ctx = Context(1)
     ctx.set_scene(sc)
