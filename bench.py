@@ -61,6 +61,10 @@ def parse():
     ap.add_argument("--rank0-codec", action="store_true",
                     help="N>1 tiles: rank 0 encodes and decodes its own bands too (instead of rendering them "
                          "straight into its frames); the one-process rehearsal uses it to exercise the codec")
+    ap.add_argument("--compositor", choices=["auto", "on", "off"], default="auto",
+                    help="N>1 tiles: rank 0 traces nothing and assembles the frames that ranks 1..N-1 "
+                         "trace as a band world of N-1 (auto: N >= 8, where rank 0's own share plus the "
+                         "decode of the others' made it the slowest rank)")
     ap.add_argument("--dist-path", action="store_true",
                     help="rehearsal: run the N>1 band/gather path even with one process (RCCL world of 1)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
@@ -189,7 +193,11 @@ def main():
                     done += m
     else:
         from raytracer_hip.dist import BandGather, BatchedBandGather, RowBands
-        rb = RowBands(W, H, args.band_rows, rank, world)
+        comp = (args.band_format == "tiles" and not args.no_pipeline and not args.rank0_codec and world >= 2
+                and (args.compositor == "on" or (args.compositor == "auto" and world >= 8)))
+        # band geometry: the process group's, or (compositor) ranks 1..N-1 as band ranks 0..N-2
+        band_rank, band_world = (max(0, rank - 1), world - 1) if comp else (rank, world)
+        rb = RowBands(W, H, args.band_rows, band_rank, band_world)
         launch_frames = 1
         px_per_launch = rb.pixels
         frame = torch.empty(W * H, dtype=torch.int32, device="cuda") if rank == 0 else None
@@ -213,16 +221,17 @@ def main():
             from raytracer_hip.dist import TileBandGather
 
             def t_encode(raw, n, wire, size, st):
-                ctx.encode_bands(W, H, rb.band_rows, rank, world, raw.data_ptr(), rb.slot_elems, n, wire.data_ptr(),
+                ctx.encode_bands(W, H, rb.band_rows, band_rank, band_world, raw.data_ptr(), rb.slot_elems, n,
+                                 wire.data_ptr(),
                                  size.data_ptr(), st.cuda_stream)
 
             def t_decode(recv, rank_stride, n, frames_, st, first_rank):
-                ctx.decode_gathered(W, H, rb.band_rows, world, recv.data_ptr(), rank_stride, n, frames_.data_ptr(),
+                ctx.decode_gathered(W, H, rb.band_rows, band_world, recv.data_ptr(), rank_stride, n, frames_.data_ptr(),
                                     W * H, st.cuda_stream, first_rank=first_rank)
 
             tg = TileBandGather(rb, torch.device("cuda", local), args.batch,
-                                lambda n: wire_layout(W, H, rb.band_rows, world, n), t_encode, t_decode,
-                                rank0_codec=args.rank0_codec)
+                                lambda n: wire_layout(W, H, rb.band_rows, band_world, n), t_encode, t_decode,
+                                rank0_codec=args.rank0_codec, compositor=comp, phys_rank=rank, phys_world=world)
             out_fmt = abi.RT_BANDS_FRAME if tg.direct else abi.RT_BANDS_INT32
             # frames alternate between trace streams (two in flight per rank); at a batch end the
             # encode runs on `stream` after the others joined it, and the trace streams then wait
@@ -248,8 +257,9 @@ def main():
                     ts = tstreams[(tg.k // tg.F) % len(tstreams)]
                     if tg.k % tg.F == 0:
                         tg.begin_batch([ts])
-                    ctx.render_bands_batch(W, H, rb.band_rows, rank, world, m, tg.target().data_ptr(), stride_b,
-                                           out_fmt, ts.cuda_stream)
+                    if not tg.idle:  # (the compositor rank only assembles)
+                        ctx.render_bands_batch(W, H, rb.band_rows, band_rank, band_world, m, tg.target().data_ptr(),
+                                               stride_b, out_fmt, ts.cuda_stream)
                     end = (tg.k + m) % tg.F == 0
                     if end and ts is not stream:
                         stream.wait_stream(ts)
@@ -391,7 +401,8 @@ def main():
                 "lights": len(sc.lights), "depth": sc.recursion_limit + 1,
                 "parallelism": (f"single GPU, {max(1, args.frames_per_launch)} frames per launch, "
                                 f"{max(1, args.inflight)} launches in flight") if not distributed else
-                f"interleaved {args.band_rows}-row bands x {world} ranks + RCCL gather to rank 0"
+                f"interleaved {args.band_rows}-row bands x {world - 1 if comp else world} ranks + RCCL gather to "
+                f"rank 0{' (compositor: rank 0 decodes, ranks 1..N-1 trace)' if comp else ''}"
                 + (" (one gather per frame)" if args.no_pipeline else
                    f" ({args.batch} frames per gather, {args.band_format} bands, double-buffered: the gather of "
                    f"one batch overlaps the trace of the next)"),

@@ -156,7 +156,8 @@ def run_batched(rank, world, port, cfg, width, height, band_rows, frames, per_ba
         dist.destroy_process_group()
 
 
-def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batch, result_path, rank0_codec=False):
+def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batch, result_path, rank0_codec=False,
+              compositor=False):
     """bench.py's default N>1 step: F frames per batch, tile-encoded band sets (host mirror of
     rt_encode_bands), size all_reduce + gather, rank 0 decodes every frame (host mirror of
     rt_decode_gathered) and checks it against the oracle."""
@@ -181,12 +182,14 @@ def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batc
             sc.camera = ((0.0, 0.0, 0.0), 0.04 * k - 0.1, -0.02 * k)
             return sc
 
-        rb = RowBands(width, height, band_rows, rank, world)
+        # compositor: ranks 1..N-1 are band ranks 0..N-2 of a band world of N-1, rank 0 only decodes
+        brank, bworld = (max(0, rank - 1), world - 1) if compositor else (rank, world)
+        rb = RowBands(width, height, band_rows, brank, bworld)
         got = {}
         batch_of = []  # frame index of every decoded frame slot, in decode order
 
         def encode(raw, n, wire, size, _stream):
-            b = tilecodec.encode(raw.numpy()[:n * rb.slot_elems], width, height, band_rows, rank, world, n)
+            b = tilecodec.encode(raw.numpy()[:n * rb.slot_elems], width, height, band_rows, brank, bworld, n)
             wire.numpy()[:len(b)] = np.frombuffer(b, dtype=np.uint8)
             size[0] = len(b)
 
@@ -195,22 +198,26 @@ def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batc
         def decode(recv, rank_stride, n, frames_, _stream, first_rank):
             host = recv.numpy()
             fr = frames_.numpy().reshape(-1, height, width)
-            for r in range(first_rank, world):
+            for r in range(first_rank, bworld):
                 tilecodec.decode_into(fr[:n], host[r * rank_stride:(r + 1) * rank_stride], width, height,
-                                      band_rows, r, world)
+                                      band_rows, r, bworld)
             for f in range(n):
                 got[decoded[0] + f] = fr[f].copy()
                 fr[f] = -7  # the ring slot is reused: stale pixels must not pass
             decoded[0] += n
 
-        g = TileBandGather(rb, "cpu", per_batch, lambda n: tilecodec.layout(width, height, band_rows, world, n),
-                           encode, decode, rank0_codec=rank0_codec)
+        g = TileBandGather(rb, "cpu", per_batch, lambda n: tilecodec.layout(width, height, band_rows, bworld, n),
+                           encode, decode, rank0_codec=rank0_codec, compositor=compositor, phys_rank=rank,
+                           phys_world=world)
         if rank == 0:
             for ring in g.frames:
                 ring.fill_(-7)
         for k in range(frames):
             if k % g.F == 0:
                 g.begin_batch()
+            if g.idle:  # the compositor rank renders nothing
+                g.commit()
+                continue
             dst = g.target().numpy()
             if g.direct:  # rank 0 renders its bands into their frame rows
                 dst = dst.reshape(height, width)

@@ -263,28 +263,47 @@ class TileBandGather:
     `decode(gathered, rank_stride, n_frames, frames, stream, first_rank)` do the codec work (the
     HIP library on GPUs, the host mirror in tests).  Rank 0's decoded frames of batch b are in
     `frames[b % 3]` (F frames, row-major) once stage C of b has run (`ring_of`).
+
+    Compositor mode (`compositor=True`; bench.py at N >= 8): rank 0 traces nothing and only
+    assembles -- it decodes every band set of each frame, which ranks 1..N-1 trace as a band
+    world of N-1 (`rb` is then the band geometry: band rank = rank - 1, band world = N - 1;
+    `phys_rank`/`phys_world` are the process group's).  At N = 8 rank 0's own 1/8 share of a
+    1080p frame (≈3 µs) plus the decode of the other 7/8 (≈2 µs) made it the slowest rank;
+    without the trace the slowest rank traces and encodes 1/7.  Rank 0 still
+    takes part in both collectives (size 0; its own gather slot is receive slot N-1, scratch).
     """
 
-    def __init__(self, rb: RowBands, device, frames_per_batch, layout_fn, encode, decode, rank0_codec=False):
+    def __init__(self, rb: RowBands, device, frames_per_batch, layout_fn, encode, decode, rank0_codec=False,
+                 compositor=False, phys_rank=None, phys_world=None):
         import torch
         self.rb, self.F, self.device = rb, max(1, frames_per_batch), torch.device(device)
         self.cuda = self.device.type == "cuda"
         self.layout_fn, self.encode, self.decode = layout_fn, encode, decode
-        self.first_rank = 0 if rank0_codec else 1
-        self.direct = rb.rank == 0 and not rank0_codec  # rank 0 renders into its frames
+        self.compositor = bool(compositor)
+        self.prank = rb.rank if phys_rank is None else int(phys_rank)
+        self.pworld = rb.world if phys_world is None else int(phys_world)
+        if self.compositor and (self.pworld != rb.world + 1 or (self.prank > 0 and rb.rank != self.prank - 1)):
+            raise ValueError("compositor mode: the band world is N-1 and band rank = rank-1")
+        if not self.compositor and (self.pworld != rb.world or self.prank != rb.rank):
+            raise ValueError("band geometry and process group differ outside compositor mode")
+        self.root = self.prank == 0
+        self.first_rank = 0 if (rank0_codec or self.compositor) else 1
+        self.direct = self.root and not rank0_codec and not self.compositor  # rank 0 renders into its frames
+        self.idle = self.root and self.compositor  # rank 0 only assembles
         self.slot_elems = rb.slot_elems
         lay = layout_fn(self.F)
         self.rank_stride = (int(lay.max_bytes) + 255) // 256 * 256
         self.raw = ([torch.zeros(self.F * self.slot_elems, dtype=torch.int32, device=self.device) for _ in range(2)]
-                    if not self.direct else None)
+                    if not (self.direct or self.idle) else None)
         self.wire = [torch.zeros(self.rank_stride, dtype=torch.uint8, device=self.device) for _ in range(3)]
         self.size = [torch.zeros(1, dtype=torch.int64, device=self.device) for _ in range(3)]
         self.size_host = torch.zeros(3, dtype=torch.int64, pin_memory=self.cuda)
-        self.recv = ([torch.zeros(rb.world * self.rank_stride, dtype=torch.uint8, device=self.device)
-                      for _ in range(2)] if rb.rank == 0 else [None, None])
+        # physical rank r's receive slot: r (compositor: its band rank r-1; rank 0's own: slot N-1)
+        self.recv = ([torch.zeros(self.pworld * self.rank_stride, dtype=torch.uint8, device=self.device)
+                      for _ in range(2)] if self.root else [None, None])
         self.frame_elems = rb.width * rb.height
         self.frames = ([torch.zeros(self.F * self.frame_elems, dtype=torch.int32, device=self.device)
-                        for _ in range(3)] if rb.rank == 0 else None)
+                        for _ in range(3)] if self.root else None)
         if self.cuda:
             self.comm, self.dec = torch.cuda.Stream(self.device), torch.cuda.Stream(self.device)
         self.k = 0             # frames rendered
@@ -301,6 +320,8 @@ class TileBandGather:
 
     def target(self, k=None):
         k = self.k if k is None else k
+        if self.idle:
+            raise RuntimeError("the compositor rank traces nothing")
         if self.direct:
             o = (k % self.F) * self.frame_elems
             return self.frames[(k // self.F) % 3][o:o + self.frame_elems]
@@ -336,8 +357,8 @@ class TileBandGather:
             ev = self.gathered_ev.pop(b - 3)
             if self.cuda:
                 main.wait_event(ev)
-        if self.direct:
-            self.size[i].zero_()  # nothing to ship: rank 0's bands are already in its frames
+        if self.direct or self.idle:
+            self.size[i].zero_()  # nothing to ship: rank 0's bands are in its frames (or it has none)
         else:
             self.encode(self.raw[b % 2], n_frames, self.wire[i], self.size[i], main)
         work = dist.all_reduce(self.size[i], op=dist.ReduceOp.MAX, async_op=True)
@@ -366,8 +387,9 @@ class TileBandGather:
         self.bytes_sent += n
         j = b % 2
         glist = None
-        if self.rb.rank == 0:
-            glist = [self.recv[j][r * self.rank_stride:r * self.rank_stride + n] for r in range(self.rb.world)]
+        if self.root:
+            slot = [(r - 1) % self.pworld if self.compositor else r for r in range(self.pworld)]
+            glist = [self.recv[j][q * self.rank_stride:q * self.rank_stride + n] for q in slot]
         if self.cuda:
             with torch.cuda.stream(self.comm):
                 if b - 2 in self.decoded_ev:  # receive buffer j was last read by decode b-2
@@ -388,7 +410,7 @@ class TileBandGather:
                 ev = torch.cuda.Event()
                 ev.record(self.dec)
                 self.gathered_ev[b] = ev
-                if self.rb.rank == 0:
+                if self.root:
                     self.decode(self.recv[b % 2], self.rank_stride, n_frames, self.ring_of(b), self.dec,
                                 self.first_rank)
                     dv = torch.cuda.Event()
@@ -397,10 +419,10 @@ class TileBandGather:
         else:
             gw.wait()
             self.gathered_ev[b] = None
-            if self.rb.rank == 0:
+            if self.root:
                 self.decode(self.recv[b % 2], self.rank_stride, n_frames, self.ring_of(b), None, self.first_rank)
                 self.decoded_ev[b] = None
-        if self.rb.rank == 0:
+        if self.root:
             self.decoded += 1
 
     def commit(self, main=None):
