@@ -15,5 +15,5 @@ step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
 step pytest_gpu 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread
 step bench_C2 300 python bench.py
 for c in C3 C4 C5; do step bench_$c 300 python bench.py --config $c --no-cpu-baseline; done
-DIST_RUNS="tiles:16 rgb24:8" step dist 300 bash tools/dist_rehearsal.sh
+DIST_RUNS="tiles:64 rgb24:8" step dist 300 bash tools/dist_rehearsal.sh
 cat gpurun_out/dist.log
