@@ -889,7 +889,16 @@ __device__ __forceinline__ Hit terminal_direct(const LaunchParams& p, f3 o, f3 d
 
 // DIRECT kernel: each lane walks its own chain with per-lane (divergent) control flow.
 template <int K, bool SCRATCH, bool GPOW, int SMAX>
+// RT_PRIO (experiment): issue priority by phase.  > 0 raises it as a wave reaches its later
+// phases (1: for the backward fold; 2: 1 after the primary segment, 2 for the fold) -- older
+// waves win VALU arbitration even more than by age (C2 +15 %, C3 +9…17 %: rejected).  < 0 gives
+// young waves the priority instead (-1: 1 until the primary segment is done; -2: 2 until then,
+// 1 through the walk, 0 for the fold).
+#ifndef RT_PRIO
+#define RT_PRIO 0
+#endif
 __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p) {
+    if constexpr (RT_PRIO < 0) __builtin_amdgcn_s_setprio(-RT_PRIO);
     constexpr int LDS_LEVELS = StackFor<K, SCRATCH>::lds_levels;  // LdsStack slots, else unused
     __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
     __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * WG_THREADS : 1];
@@ -919,6 +928,8 @@ __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p
         stk.origin(d);
         f3 leaf = mk(0.0f, 0.0f, 0.0f);
         Hit h = nearest_direct<true, SMAX>(p, o, d, pmask);
+        if constexpr (RT_PRIO >= 2 || RT_PRIO == -2) __builtin_amdgcn_s_setprio(1);
+        if constexpr (RT_PRIO == -1) __builtin_amdgcn_s_setprio(0);
         int count = 0;
         for (;;) {
             if (h.prim == HIT_NONE) break;      // nothing hit: plane colour stays Zero
@@ -951,6 +962,8 @@ __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p
                 col.x += ra.w;
             }
         }
+        if constexpr (RT_PRIO >= 1) __builtin_amdgcn_s_setprio(RT_PRIO >= 2 ? 2 : 1);
+        if constexpr (RT_PRIO == -2) __builtin_amdgcn_s_setprio(0);
         while (RT_ABLATE != 1 && stk.n > 0) {
             float4 ra, rb;
             stk.pop(p, ra, rb);
