@@ -160,6 +160,7 @@ def main():
         pass
 
     streams = [stream]
+    comp = False  # N>1 compositor mode (rank 0 only assembles)
     tg = None  # tile-encoded gather (N > 1, --band-format tiles)
     run = None  # run(n): n steps (frames); else one step() per frame
     if not distributed:
@@ -380,7 +381,7 @@ def main():
         traffic = pmc["hbm_bytes_per_launch"] / pmc_frames * launch_frames if pmc else None
         valu_insts = (pmc.get("counters") or {}).get("SQ_INSTS_VALU") if pmc else None
         valu_frame = valu_insts / pmc_frames if valu_insts else None  # wave instructions per frame
-        brute_tops = (f_alg / steps / max(1, world)) * launch_frames / kernel_s / 1e12
+        brute_tops = (f_alg / steps / max(1, world - 1 if comp else world)) * launch_frames / kernel_s / 1e12
         out = {
             "metric": METRIC,
             "value": rays / elapsed / 1e6,
@@ -434,7 +435,7 @@ def main():
                 "frac": valu_frame * 64 / period_s / 1e12 / VALU_PEAK_TOPS if valu_frame else None,
                 "achieved_per_launch": valu_frame * launch_frames * 64 / kernel_s / 1e12 if valu_frame else None,
                 "brute_force_equiv": brute_tops,
-                "brute_force_ops_per_launch": f_alg / steps / max(1, world) * launch_frames,
+                "brute_force_ops_per_launch": f_alg / steps / max(1, world - 1 if comp else world) * launch_frames,
                 "note": "achieved = issued VALU lane-ops per frame (profiles/pmc_traffic.json SQ_INSTS_VALU x 64) / "
                         "frame period; achieved_per_launch uses the launch duration instead; brute_force_equiv = "
                         "24 ops per sphere test + 17 per plane test over every primitive (SURVEY.md 8d) / kernel "
