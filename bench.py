@@ -34,8 +34,9 @@ OPS_PER_PLANE_TEST = 17        # ... of IntersectPlane
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1000)
-    ap.add_argument("--warmup", type=int, default=200,
+    ap.add_argument("--steps", type=int, default=1024,
+                    help="timed frames (default: 64 launches of the default 16 frames)")
+    ap.add_argument("--warmup", type=int, default=256,
                     help="untimed frames first: the GPU needs ~10 ms of load to reach steady clocks")
     ap.add_argument("--config", default="C2")
     ap.add_argument("--size", default="",

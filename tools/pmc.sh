@@ -2,8 +2,9 @@
 # PMC passes on the trace kernel, one counter group per rocprofv3 run (gfx950 rules:
 # FETCH_SIZE and WRITE_SIZE in separate passes; never combined with tracing domains).
 # Usage (GPU box): bash tools/pmc.sh CONFIG [extra bench args]
-# bench.py's default launches of 16 frames: warmup and steps are multiples of 16, so every
-# dispatch covers 16 frames (pmc_summary.py --frames-per-launch 16).
+# Dispatches of 16 frames (--frames-per-launch 16; warmup and steps multiples of 16), so every
+# dispatch covers 16 frames (pmc_summary.py --frames-per-launch 16); bench.py scales the
+# per-frame counts to its own launch size.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
@@ -18,7 +19,7 @@ for group in "FETCH_SIZE" "WRITE_SIZE" "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_
     i=$((i+1))
     echo "== pass $i: $group"
     timeout -k 10 300 rocprofv3 --pmc $group --output-format csv -d "$OUT/p$i" -o run \
-        -- python3 bench.py --config "$CFG" --steps ${PMC_STEPS:-32} --warmup 16 --no-cpu-baseline --no-tick "$@" > "$OUT/p$i.log" 2>&1
+        -- python3 bench.py --config "$CFG" --steps ${PMC_STEPS:-32} --warmup 16 --no-cpu-baseline --no-tick --frames-per-launch 16 "$@" > "$OUT/p$i.log" 2>&1
     rc=$?
     echo "rc=$rc"
     if [ $rc -ne 0 ] && grep -qiE "memory access fault|segmentation|core dumped" "$OUT/p$i.log"; then exit $rc; fi

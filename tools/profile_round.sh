@@ -16,7 +16,7 @@ for cfg in "$@"; do
         --frames-per-launch 16 > "gpurun_out/pmc_${cfg}_summary.txt"
     rm -rf "gpurun_out/trace_$cfg"
     timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "gpurun_out/trace_$cfg" -o run \
-        -- python3 bench.py --config "$cfg" --steps 320 --warmup 48 --no-cpu-baseline --no-tick > "gpurun_out/trace_$cfg.log" 2>&1
+        -- python3 bench.py --config "$cfg" --steps 320 --warmup 64 --no-cpu-baseline --no-tick > "gpurun_out/trace_$cfg.log" 2>&1
     rc=$?; echo "trace $cfg rc=$rc"; [ $rc -eq 0 ] || exit $rc
     extra=""; [ "$cfg" = "C2" ] || extra="--no-cpu-baseline"
     timeout -k 10 300 python3 bench.py --config "$cfg" --pmc gpurun_out/pmc_traffic.json $extra > "gpurun_out/bench_$cfg.json" 2> "gpurun_out/bench_$cfg.err"
