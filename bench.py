@@ -4,13 +4,21 @@
 One step = one frame of the per-pixel trace (RayTracer.Tick, Raytracer/RayTracer.cs:886-935)
 on the configuration named by --config (default C2 = BASELINE.json configs[1]: 1920x1080,
 8 spheres + 1 plane, 1 light, depth 1), with the scene resident in HBM and the frame written
-to HBM.  N > 1 (one process per GPU under torch.distributed.run): the frame is split into
-interleaved 8-row bands, band b on rank b % N, and the bands are gathered to rank 0 over
-RCCL (torch.distributed backend "nccl" is RCCL on ROCm) and scattered into the frame there --
-strong scaling of a fixed frame.
+to HBM.
+
+N = 1: the timed frames run as balanced launches of up to 64 frames (rt_render_bands_batch),
+one launch in flight, every launch timed alone with a HIP event pair (roofline.kernel_avg_ms,
+which rocprofv3's kernel trace of the same command reproduces).  C3 (the north-star config:
+depth 4, 2 lights) is measured in the same run ("also").
+
+N > 1 (`--gpus N`: one process per GPU; started here through torch.distributed.run when no
+launcher set WORLD_SIZE): the frame is split into interleaved 8-row bands, band b on rank
+b % N, and the band sets are gathered to rank 0 over RCCL (torch.distributed backend "nccl"
+is RCCL on ROCm) -- strong scaling of a fixed frame.
 
 Prints ONE JSON line (rank 0).  Rays = primary + reflected + shadow rays of the visible
-(nearest-hit) path, counted by the kernel itself (rt_get_stats).
+(nearest-hit) path, counted by the kernel itself (rt_get_stats); `work_per_frame` sets the
+tests the kernels actually executed beside those nominal counts.
 """
 import argparse
 import json
@@ -31,23 +39,31 @@ OPS_PER_SPHERE_TEST = 24       # miss-path binary32 ops of Inter
 OPS_PER_PLANE_TEST = 17        # ... of IntersectPlane
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=1024,
-                    help="timed frames (default: 64 launches of the default 16 frames)")
-    ap.add_argument("--warmup", type=int, default=256,
-                    help="untimed frames first: the GPU needs ~10 ms of load to reach steady clocks")
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one process per GPU).  Without a torch.distributed launcher (no WORLD_SIZE) and "
+                         "N > 1, bench.py starts the N ranks itself (torch.distributed.run); every rank checks "
+                         "WORLD_SIZE == N")
+    ap.add_argument("--steps", type=int, default=1024, help="timed frames")
+    ap.add_argument("--warmup", type=int, default=256, help="untimed frames first")
+    ap.add_argument("--min-warmup-ms", type=float, default=50.0,
+                    help="N=1: keep warming up (untimed, whole launches) until this much wall time has passed -- "
+                         "the GPU needs ~10-50 ms of load to reach its steady clock; reported as warmup_effective")
     ap.add_argument("--config", default="C2")
+    ap.add_argument("--also", default="C3",
+                    help="N=1: comma list of further configs measured in the same run and reported under 'also' "
+                         "(default C3, the north-star config: depth 4, 2 lights); '' = none")
     ap.add_argument("--size", default="",
                     help="WxH: probe runs only -- the config's scene at another frame size (never the bench line)")
     ap.add_argument("--band-rows", type=int, default=8)
-    ap.add_argument("--frames-per-launch", type=int, default=16,
-                    help="N=1: frames traced per launch (rt_render_bands_batch; every frame in full, the same "
-                         "camera); 1 = one rt_render_device launch per frame.  N>1 tiles: = --batch")
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="launches in flight (a swap chain: one stream and one output buffer per launch "
-                         "slot; every frame is fully traced)")
+    ap.add_argument("--frames-per-launch", type=int, default=64,
+                    help="N=1: at most this many frames per launch (rt_render_bands_batch: every frame traced in "
+                         "full, the same camera); the steps are split into balanced launches (20 -> one of 20, "
+                         "100 -> 50 + 50).  N>1 tiles: = --batch")
+    ap.add_argument("--inflight", type=int, default=1,
+                    help="launches in flight (a swap chain: one stream and one output buffer per slot).  1 (default): "
+                         "every launch is timed alone with a HIP event pair, so kernel time x launches <= wall time")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="N>1: gather each frame before tracing the next (no double buffering)")
     ap.add_argument("--batch", type=int, default=0,
@@ -68,13 +84,46 @@ def parse():
                          "decode of the others' made it the slowest rank)")
     ap.add_argument("--dist-path", action="store_true",
                     help="rehearsal: run the N>1 band/gather path even with one process (RCCL world of 1)")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--verify", action="store_true",
+                    help="N>1 path: after the timed run rank 0 compares every frame still in its frame rings (tiles) "
+                         "with a single-launch render of the same view; exit 3 on a mismatch")
+    ap.add_argument("--master-port", type=int, default=29531, help="self-launch (--gpus N > 1): rendezvous port")
+    ap.add_argument("--cpu-seconds", type=float, default=20.0,
+                    help="CPU baseline budget: about half on the bench config, the rest on C1 and the verbatim "
+                         "reference scene")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-tick", action="store_true",
-                    help="skip the Tick()-path probe (profiling runs: keeps every trace dispatch the same size)")
+                    help="skip the Tick()-path probe and the work count (profiling runs: every trace dispatch of "
+                         "the run then has the bench's launch shape)")
     ap.add_argument("--pmc", default=os.path.join(ROOT, "profiles", "pmc_traffic.json"),
                     help="rocprofv3 PMC summary (HBM bytes per trace launch) for roofline.traffic")
-    return ap.parse_args()
+    return ap.parse_args(argv)
+
+
+def launch_command(argv, n, port):
+    """The torch.distributed.run command line that starts n ranks of this script with argv."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+            "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + list(argv)
+
+
+def world_check(args, env=os.environ):
+    """(action, message): 'run' in this process, 'spawn' the ranks, or 'fail'.
+
+    Under a launcher every rank must see WORLD_SIZE == --gpus; without one, --gpus N > 1 spawns N
+    ranks (the parent touches no GPU: it only counts devices, which does not initialise HIP)."""
+    if "WORLD_SIZE" in env:
+        world = int(env["WORLD_SIZE"])
+        if world != args.gpus:
+            return "fail", f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}"
+        return "run", ""
+    if args.gpus <= 1:
+        return "run", ""
+    return "spawn", ""
+
+
+def device_count():
+    import torch
+    return torch.cuda.device_count()
 
 
 def cpu_model():
@@ -87,32 +136,62 @@ def cpu_model():
     return platform.processor()
 
 
-def cpu_baseline(scene, rays_per_frame, seconds):
+def cgroup_cpus():
+    """CPU quota of this process's cgroup (cgroup v2 cpu.max), or None when unlimited/unknown."""
+    try:
+        quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if quota == "max" else float(quota) / float(period)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(samples, seconds):
     """Reference-faithful CPU restatement (oracle, all-hit driver, column-outer/row-parallel loop
-    like RayTracer.cs:898-901), timed on this host's cores on whole frames of the same workload."""
+    like RayTracer.cs:898-901), timed on every core this process may run on, on whole frames.
+
+    samples: [(scene, rays_per_frame, share of `seconds`)].  The first is the bench workload
+    (the cpu_baseline value); the others are reported beside it."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import pyoracle
-    threads = max(1, min(16, os.cpu_count() or 1))
-    pyoracle.render(scene.resized(scene.width, 8), pyoracle.MODE_REFERENCE, threads)  # warm-up
-    times = []
-    t_start = time.perf_counter()
-    while True:
-        t0 = time.perf_counter()
-        pyoracle.render(scene, pyoracle.MODE_REFERENCE, threads)
-        times.append(time.perf_counter() - t0)
-        if time.perf_counter() - t_start > seconds and len(times) >= 2:
-            break
-        if len(times) >= 50:
-            break
-    times.sort()
-    med = times[len(times) // 2]
-    return {
-        "value": rays_per_frame / med / 1e6, "unit": "Mray/s", "cores": threads, "kind": "port",
-        "fps": 1.0 / med,
-        "sample": f"{len(times)} full {scene.width}x{scene.height} frames of {scene.name} (median), "
-                  f"C restatement of RayTracer.cs (all-hit shading, per-pixel camera trig, column-outer/"
-                  f"row-parallel loop), {threads} threads on {cpu_model()}",
-    }
+    affinity = len(os.sched_getaffinity(0))
+    quota = cgroup_cpus()
+    # every CPU this process may use: its affinity set, capped by its cgroup's CPU quota (a GPU box
+    # grants a 16-CPU share of a larger machine: more threads than the quota only get throttled)
+    threads = max(1, min(affinity, int(quota + 0.5))) if quota else affinity
+    out = None
+    for scene, rays_per_frame, share in samples:
+        if rays_per_frame is None:  # count the visible-path rays with the oracle's nearest driver
+            _, ost = pyoracle.render(scene, pyoracle.MODE_NEAREST, threads)
+            rays_per_frame = ost["primary_rays"] + ost["reflect_rays"] + ost["shadow_rays"]
+        pyoracle.render(scene.resized(scene.width, 8), pyoracle.MODE_REFERENCE, threads)  # warm-up
+        times = []
+        t_start = time.perf_counter()
+        while True:
+            t0 = time.perf_counter()
+            pyoracle.render(scene, pyoracle.MODE_REFERENCE, threads)
+            times.append(time.perf_counter() - t0)
+            if (time.perf_counter() - t_start > seconds * share and len(times) >= 3) or len(times) >= 200:
+                break
+        times.sort()
+        med = times[len(times) // 2]
+        entry = {"value": rays_per_frame / med / 1e6, "unit": "Mray/s", "fps": 1.0 / med, "frames": len(times),
+                 "workload": f"{scene.name}: {scene.width}x{scene.height}, {len(scene.spheres)} spheres, "
+                             f"{len(scene.lights)} lights, depth {scene.recursion_limit + 1}"}
+        if out is None:
+            out = dict(entry)
+            out.update({
+                "cores": threads, "kind": "port", "affinity_cpus": affinity, "nproc": os.cpu_count(),
+                "cgroup_cpu_quota": quota,
+                "sample": f"{len(times)} full {scene.width}x{scene.height} frames of {scene.name} (median), C "
+                          f"restatement of RayTracer.cs (all-hit shading, per-pixel camera trig, column-outer/"
+                          f"row-parallel loop), {threads} threads = every CPU this process may use "
+                          f"(sched_getaffinity {affinity} CPUs, cgroup quota {quota if quota else 'none'} CPUs, "
+                          f"os.cpu_count {os.cpu_count()}) on {cpu_model()}",
+                "others": {},
+            })
+        else:
+            out["others"][scene.name] = entry
+    return out
 
 
 def load_pmc(path, config, world):
@@ -125,8 +204,101 @@ def load_pmc(path, config, world):
         return None
 
 
+def plan_launches(n, fpl):
+    """Balanced launch sizes for n frames, at most fpl per launch (20 -> [20], 100 -> [50, 50])."""
+    if n <= 0:
+        return []
+    k = -(-n // fpl)
+    base, extra = divmod(n, k)
+    return [base + 1] * extra + [base] * (k - extra)
+
+
+def measure_single(ctx, sc, args, torch, abi, steps, warmup):
+    """N = 1: `steps` frames of `sc` in balanced launches of <= --frames-per-launch frames
+    (rt_render_bands_batch: one launch, grid z = frame, every frame traced in full into its own
+    slot), --inflight launches in flight.  Timed between two torch.cuda.synchronize() calls."""
+    W, H = sc.width, sc.height
+    nf = max(1, args.inflight)
+    fpl = max(1, min(args.frames_per_launch, 65535))
+    cap = max(plan_launches(steps, fpl) + plan_launches(max(1, warmup), fpl))
+    bufs = [torch.empty(cap * W * H, dtype=torch.int32, device="cuda") for _ in range(nf)]
+    stream = torch.cuda.current_stream()
+    streams = [stream] + [torch.cuda.Stream() for _ in range(nf - 1)]
+    k = [0]
+
+    def issue(n, lim=fpl):
+        for m in plan_launches(n, min(lim, cap)):
+            if not 1 <= m <= cap:  # every launch must fit its output slot
+                raise RuntimeError(f"launch of {m} frames exceeds the {cap}-frame buffer")
+            i = k[0] % nf
+            k[0] += 1
+            ctx.render_bands_batch(W, H, H, 0, 1, m, bufs[i].data_ptr(), W * H * 4, abi.RT_BANDS_INT32,
+                                   streams[i].cuda_stream)
+
+    # one launch in flight: an event pair around every launch measures that launch alone
+    ctx.set_timing(1 if nf == 1 else 4)
+    t_w = time.perf_counter()
+    issue(warmup)
+    torch.cuda.synchronize()
+    done = warmup
+    while (time.perf_counter() - t_w) * 1e3 < args.min_warmup_ms:  # clock ramp (untimed)
+        per_frame = (time.perf_counter() - t_w) / max(1, done)
+        n = max(1, min(16 * fpl, int((args.min_warmup_ms / 1e3 - (time.perf_counter() - t_w)) / per_frame) + 1))
+        issue(n)
+        done += n
+        torch.cuda.synchronize()
+    ctx.reset_stats()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)  # on the launch stream(s): the others start after it, it ends after them
+    for s in streams[1:]:
+        s.wait_event(ev0)
+    issue(steps)
+    host_s = (time.perf_counter() - t0) / max(1, steps)  # host issue time per step
+    for s in streams[1:]:
+        stream.wait_stream(s)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    st = ctx.stats()
+    return {"elapsed": elapsed, "period_s": ev0.elapsed_time(ev1) / 1e3 / steps, "stats": st, "host_s": host_s,
+            "launches": len(plan_launches(steps, fpl)), "warmup_effective": done, "inflight": nf}
+
+
+def single_summary(sc, m, steps):
+    """Per-config numbers of an N = 1 measurement (value, roofline inputs)."""
+    st = m["stats"]
+    rays = st["primary_rays"] + st["reflect_rays"] + st["shadow_rays"]
+    W, H = sc.width, sc.height
+    launches = m["launches"]
+    frames_per_launch = steps / launches
+    kernel_s = st["kernel_ms"] / 1e3 / max(1, st["timed_launches"]) if st["timed_launches"] else m["period_s"]
+    achieved = 4.0 * W * H * frames_per_launch / kernel_s / 1e9
+    return {
+        "value": rays / m["elapsed"] / 1e6, "unit": "Mray/s", "ms_per_step": m["elapsed"] * 1e3 / steps,
+        "fps": steps / m["elapsed"], "rays_per_frame": rays / steps,
+        "workload": f"{sc.name}: {sc.note}", "kernel": "trace_direct_kernel" if len(sc.spheres) < 12
+        else "trace_bundle_kernel",
+        "kernel_avg_ms": kernel_s * 1e3, "kernel_ms_per_frame": kernel_s * 1e3 / frames_per_launch,
+        "frames_per_launch": frames_per_launch, "launches": launches, "timed_launches": st["timed_launches"],
+        "frame_period_ms": m["period_s"] * 1e3, "hbm_gbs": achieved, "hbm_frac": achieved / HBM_PEAK_GBS,
+        "f_alg": OPS_PER_SPHERE_TEST * st["sphere_tests"] + OPS_PER_PLANE_TEST * st["plane_tests"],
+    }
+
+
 def main():
     args = parse()
+    action, msg = world_check(args)
+    if action == "fail":
+        print(msg, file=sys.stderr, flush=True)
+        sys.exit(2)
+    if action == "spawn":
+        n = device_count()
+        if n < args.gpus:
+            print(f"bench.py --gpus {args.gpus}: only {n} GPU(s) visible", file=sys.stderr, flush=True)
+            sys.exit(2)
+        sys.exit(subprocess.call(launch_command(sys.argv[1:], args.gpus, args.master_port)))
     if args.batch <= 0:
         args.batch = 64 if args.steps >= 256 else max(8, args.steps // 4)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -139,14 +311,18 @@ def main():
     if not os.path.exists(abi.LIB_PATH):
         subprocess.run(["make", "-s", "-C", os.path.join(PKG, "csrc")], check=True)
 
-    distributed = world > 1 or args.dist_path
-    if distributed:
-        torch.cuda.set_device(local)
-        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        os.environ.setdefault("MASTER_PORT", "29531")
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(0)
+    if world == 1 and not args.dist_path:
+        return main_single(args, torch, Context, abi, scenes)
+
+    # N > 1 (or the one-process rehearsal of that path): one process per GPU, RCCL process group
+    torch.cuda.set_device(local)
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29531")
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    if args.band_format == "tiles" and not args.no_pipeline and args.inflight > 2:
+        # the next-but-one batch reuses raw[b % 2]: with a third trace stream it could overwrite the
+        # band set that encode(b) still reads
+        raise SystemExit("bench.py: the tile pipeline supports --inflight 1 or 2")
     sc = scenes.config(args.config)
     if args.size:
         w_, h_ = map(int, args.size.lower().split("x"))
@@ -161,39 +337,11 @@ def main():
         pass
 
     streams = [stream]
-    comp = False  # N>1 compositor mode (rank 0 only assembles)
-    tg = None  # tile-encoded gather (N > 1, --band-format tiles)
+    tg = None  # tile-encoded gather (--band-format tiles)
     run = None  # run(n): n steps (frames); else one step() per frame
-    if not distributed:
-        nf = max(1, args.inflight)
-        fpl = max(1, args.frames_per_launch)
-        frames = [torch.empty(fpl * W * H, dtype=torch.int32, device="cuda") for _ in range(nf)]
-        fptr = [f.data_ptr() for f in frames]
-        streams += [torch.cuda.Stream() for _ in range(nf - 1)]
-        sptr = [st_.cuda_stream for st_ in streams]
-        launch_frames = fpl
-        px_per_launch = fpl * W * H
-        k_step = [0]
-
-        def step():
-            # frame k into slot k % nf on that slot's stream: frame k+1 fills the GPU while
-            # frame k's last waves finish
-            k = k_step[0]
-            k_step[0] = k + 1
-            ctx.render_device(W, H, fptr[k % nf], sptr[k % nf])
-
-        if fpl > 1:
-            def run(n):  # noqa: F811
-                # launches of fpl frames (each traced in full into its own buffer slot), two
-                # launches in flight on the swap-chain streams
-                done = 0
-                while done < n:
-                    m = min(fpl, n - done)
-                    i = k_step[0] % nf
-                    k_step[0] += 1
-                    ctx.render_bands_batch(W, H, H, 0, 1, m, fptr[i], W * H * 4, abi.RT_BANDS_INT32, sptr[i])
-                    done += m
-    else:
+    distributed = True
+    comp = False  # compositor mode (rank 0 only assembles)
+    if True:
         from raytracer_hip.dist import BandGather, BatchedBandGather, RowBands
         comp = (args.band_format == "tiles" and not args.no_pipeline and not args.rank0_codec and world >= 2
                 and (args.compositor == "on" or (args.compositor == "auto" and world >= 8)))
@@ -401,9 +549,7 @@ def main():
                 "workload": f"{sc.name}: {sc.note}",
                 "width": W, "height": H, "spheres": len(sc.spheres), "planes": len(sc.planes),
                 "lights": len(sc.lights), "depth": sc.recursion_limit + 1,
-                "parallelism": (f"single GPU, {max(1, args.frames_per_launch)} frames per launch, "
-                                f"{max(1, args.inflight)} launches in flight") if not distributed else
-                f"interleaved {args.band_rows}-row bands x {world - 1 if comp else world} ranks + RCCL gather to "
+                "parallelism": f"interleaved {args.band_rows}-row bands x {world - 1 if comp else world} ranks + RCCL gather to "
                 f"rank 0{' (compositor: rank 0 decodes, ranks 1..N-1 trace)' if comp else ''}"
                 + (" (one gather per frame)" if args.no_pipeline else
                    f" ({args.batch} frames per gather, {args.band_format} bands, double-buffered: the gather of "
@@ -451,24 +597,150 @@ def main():
             # wire bytes each rank shipped per frame (max over ranks, as gathered), vs the raw band set
             out["config"]["gather_wire_bytes_per_frame"] = tg.bytes_sent / steps
             out["config"]["gather_rgb24_bytes_per_frame"] = 3 * rb.slot_elems
-        if world == 1 and not args.no_tick:
-            # Tick() path for context: full frame into pinned host memory (PCIe D2H included); not `value`
-            import numpy as np
-            host = np.empty(W * H, dtype=np.int32)
-            ctx.register_host(host)
-            ctx.render(W, H, host)
-            n_tick = 20
-            t1 = time.perf_counter()
-            for _ in range(n_tick):
-                ctx.render(W, H, host)
-            out["tick_fps_incl_d2h"] = n_tick / (time.perf_counter() - t1)
-            ctx.unregister_host(host)
-            if not args.no_cpu_baseline:
-                out["cpu_baseline"] = cpu_baseline(sc, rays_per_frame, args.cpu_seconds)
+        if args.verify:
+            out["verified_frames"] = verify_rings(ctx, tg, W, H, args.steps, torch)
         print(json.dumps(out), flush=True)
     ctx.close()
     if distributed:
         dist.destroy_process_group()
+
+
+def verify_rings(ctx, tg, W, H, steps, torch):
+    """Rank 0 of the tile pipeline: every decoded frame left in the frame rings (the last
+    batches) must equal a single-launch render of the same view (all frames share the camera)."""
+    if tg is None or tg.frames is None:
+        return 0
+    want = torch.empty(W * H, dtype=torch.int32, device="cuda")
+    ctx.render_device(W, H, want.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    n = 0
+    first_timed = tg.batch - -(-steps // tg.F)  # batches of the timed run (the warm-up was drained before)
+    for b in range(max(first_timed, tg.batch - 3), tg.batch):  # the rings of the last (up to) 3 batches
+        ring = tg.ring_of(b).view(tg.F, W * H)
+        frames_in_batch = tg.F if (b < tg.batch - 1 or steps % tg.F == 0) else steps % tg.F
+        for f in range(frames_in_batch):
+            if not torch.equal(ring[f], want):
+                bad = int((ring[f] != want).sum())
+                print(f"verify: batch {b} frame {f}: {bad} pixels differ", file=sys.stderr, flush=True)
+                sys.exit(3)
+            n += 1
+    return n
+
+
+def main_single(args, torch, Context, abi, scenes):
+    """N = 1: the bench config (+ --also configs) on cuda:0; prints the JSON line."""
+    torch.cuda.set_device(0)
+    sc = scenes.config(args.config)
+    if args.size:
+        w_, h_ = map(int, args.size.lower().split("x"))
+        sc = sc.resized(w_, h_, f"{sc.name}@{w_}x{h_}")
+    W, H = sc.width, sc.height
+    steps = args.steps
+    ctx = Context(1)
+    ctx.set_scene(sc)
+    m = measure_single(ctx, sc, args, torch, abi, steps, args.warmup)
+    r = single_summary(sc, m, steps)
+    pmc = load_pmc(args.pmc, sc.name, 1)
+    # PMC summaries are per dispatch of `frames_per_launch` frames (tools/pmc.sh): per frame here
+    pmc_frames = (pmc.get("frames_per_launch") or 1) if pmc else 1
+    traffic = pmc["hbm_bytes_per_launch"] / pmc_frames * r["frames_per_launch"] if pmc else None
+    valu_insts = (pmc.get("counters") or {}).get("SQ_INSTS_VALU") if pmc else None
+    valu_frame = valu_insts / pmc_frames if valu_insts else None  # wave instructions per frame
+    kernel_frame_s = r["kernel_ms_per_frame"] / 1e3
+    isolated = m["inflight"] == 1 and r["timed_launches"] == r["launches"]
+    out = {
+        "metric": METRIC,
+        "value": r["value"],
+        "unit": "Mray/s",
+        "n_gpus": 1,
+        "steps": steps,
+        "warmup": args.warmup,
+        "warmup_effective": m["warmup_effective"],
+        "ms_per_step": r["ms_per_step"],
+        "fps": r["fps"],
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded SplitMix64 scene, BASELINE.json config; no assets needed)",
+        "config": {
+            "workload": r["workload"],
+            "width": W, "height": H, "spheres": len(sc.spheres), "planes": len(sc.planes),
+            "lights": len(sc.lights), "depth": sc.recursion_limit + 1,
+            "parallelism": f"single GPU, {r['launches']} balanced launches of <= {args.frames_per_launch} frames "
+                           f"(rt_render_bands_batch), {m['inflight']} in flight",
+            "rays_per_frame": r["rays_per_frame"],
+        },
+        "roofline": {
+            "bound": "hbm",
+            "achieved": r["hbm_gbs"],
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": r["hbm_frac"],
+            "traffic": traffic,
+            "kernel": r["kernel"],
+            "kernel_avg_ms": r["kernel_avg_ms"],
+            "frames_per_launch": r["frames_per_launch"],
+            "launches": r["launches"],
+            "kernel_ms_per_frame": r["kernel_ms_per_frame"],
+            "frame_period_ms": r["frame_period_ms"],
+            "kernel_avg_source": ("HIP event pair around every launch on its stream, one launch in flight (the "
+                                  "launch alone on the GPU, as rocprofv3's kernel trace of the same command)")
+            if isolated else "sampled HIP event pairs of overlapping launches (--inflight > 1)",
+            "note": "algorithmic bytes = 4 B framebuffer store per pixel x frames per launch; traffic = PMC "
+                    "FETCH_SIZE x 2 + WRITE_SIZE per launch (profiles/pmc_traffic.json); the path is "
+                    "FP32-VALU-bound (roofline_valu)",
+        },
+        "roofline_valu": {
+            "bound": "valu",
+            # issued VALU lane-ops (PMC SQ_INSTS_VALU x 64) per frame over the kernel time per frame
+            "achieved": valu_frame * 64 / kernel_frame_s / 1e12 if valu_frame else None,
+            "peak": VALU_PEAK_TOPS,
+            "unit": "TOP/s",
+            "frac": valu_frame * 64 / kernel_frame_s / 1e12 / VALU_PEAK_TOPS if valu_frame else None,
+            "brute_force_equiv": r["f_alg"] / steps / kernel_frame_s / 1e12,
+            "note": "achieved = issued VALU lane-ops per frame (profiles/pmc_traffic.json SQ_INSTS_VALU x 64) / "
+                    "kernel time per frame; brute_force_equiv = 24 ops per sphere test + 17 per plane test over "
+                    "every primitive (SURVEY.md 8d) / kernel time -- above peak where culling skips tests",
+        },
+        "cpu_baseline": None,
+        "host_ms_per_step": m["host_s"] * 1e3,
+    }
+    if not args.no_tick:
+        # Work actually executed (diagnostic kernels, one frame, untimed) beside the nominal counts:
+        # Mray/s counts SURVEY 8(d)'s visible-path rays, some of whose shadow tests are skipped
+        w = ctx.count_work(W, H)
+        nominal = w["primary_rays"] + w["reflect_rays"] + w["shadow_rays"]
+        out["work_per_frame"] = dict(w, rays=nominal, rays_match_timed_run=nominal == r["rays_per_frame"],
+                                     note="nominal counts (SURVEY.md 8d: every primitive of every visible-path ray) "
+                                          "vs *_run = exact tests / shadow rays the kernel executed (skipped: shadow "
+                                          "tests that cannot change the pixel, culled spheres)")
+        # Tick() path for context: full frame into pinned host memory (PCIe D2H included); not `value`
+        import numpy as np
+        host = np.empty(W * H, dtype=np.int32)
+        ctx.register_host(host)
+        ctx.render(W, H, host)
+        n_tick = 20
+        t1 = time.perf_counter()
+        for _ in range(n_tick):
+            ctx.render(W, H, host)
+        out["tick_fps_incl_d2h"] = n_tick / (time.perf_counter() - t1)
+        ctx.unregister_host(host)
+    also = [c for c in (x.strip() for x in args.also.split(",")) if c and c.upper() != sc.name.upper()]
+    if also:
+        out["also"] = {}
+        for name in also:
+            sc2 = scenes.config(name)
+            ctx.set_scene(sc2)
+            r2 = single_summary(sc2, measure_single(ctx, sc2, args, torch, abi, steps, args.warmup), steps)
+            out["also"][sc2.name] = {k: r2[k] for k in ("value", "unit", "ms_per_step", "fps", "rays_per_frame",
+                                                        "workload", "kernel", "kernel_avg_ms", "kernel_ms_per_frame",
+                                                        "frames_per_launch", "launches", "hbm_frac")}
+    if not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline([(sc, r["rays_per_frame"], 0.5), (scenes.config("C1"), None, 0.2),
+                                            (scenes.reference(512, 512), None, 0.3)], args.cpu_seconds)
+    print(json.dumps(out), flush=True)
+    ctx.close()
 
 
 if __name__ == "__main__":

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 4
+#define RT_ABI_VERSION 5
 
 /* ---- status codes ---------------------------------------------------------- */
 enum {
@@ -136,6 +136,20 @@ typedef struct rt_stats {
     uint64_t timed_gathers;  /* gathers in gather_ms                       */
 } rt_stats;
 
+/* Nominal and executed work of one frame (rt_count_work, ABI 5).  The nominal counts are
+ * SURVEY.md 8(d)'s (every primitive of every visible-path ray; Mray/s counts these rays).
+ * The kernels skip work that provably cannot change a pixel -- shadow rays whose outcome
+ * cannot matter (shadow_rays_run <= shadow_rays), sphere tests culled by screen boxes, wave
+ * bundles and the terminal-segment rule -- so the *_run counts are what actually ran: per
+ * lane, each exact IntersectsSphere / IntersectPlane evaluation whose result the lane used. */
+typedef struct rt_work {
+    uint64_t primary_rays, reflect_rays, shadow_rays;  /* nominal, as rt_stats          */
+    uint64_t sphere_tests, plane_tests;                /* nominal, as rt_stats          */
+    uint64_t shadow_rays_run;   /* shadow rays whose sphere loop ran                   */
+    uint64_t sphere_tests_run;  /* exact sphere tests executed (trace + shadow rays)   */
+    uint64_t plane_tests_run;   /* exact plane tests executed                          */
+} rt_work;
+
 typedef struct rt_ctx rt_ctx;
 
 /* ---- library / device ------------------------------------------------------- */
@@ -150,6 +164,12 @@ const char* rt_last_error(const rt_ctx* ctx);
  * RCCL communicator (ncclCommInitAll); frames are split into interleaved row bands and
  * gathered to device 0. */
 int rt_create(int n_gpus, rt_ctx** out_ctx);
+/* rt_create with flags (ABI 5).  RT_CREATE_RCCL_GATHER: rt_render takes the multi-GPU path
+ * (row bands per device, ncclCommInitAll + grouped ncclGather to device 0, one-launch
+ * reassembly) for any n_gpus, 1 included -- the path the C# shim uses with RT_GPUS > 1,
+ * exercisable on a one-GPU machine. */
+enum { RT_CREATE_RCCL_GATHER = 1 };
+int rt_create_ex(int n_gpus, int flags, rt_ctx** out_ctx);
 void rt_destroy(rt_ctx* ctx);
 
 /* ---- scene (replaces the hard-coded fields RayTracer.cs:441-490) ------------- */
@@ -294,6 +314,10 @@ int rt_debug_segments(rt_ctx* ctx, int width, int height, int sample_stride, rt_
 int rt_set_timing(rt_ctx* ctx, int every);
 int rt_get_stats(rt_ctx* ctx, rt_stats* out_stats);
 int rt_reset_stats(rt_ctx* ctx);
+/* Traces one width x height frame of the current camera with the diagnostic kernels (same
+ * pixels, plus executed-work tallies) into a context-owned buffer and returns its work.
+ * Synchronous; single-GPU contexts; does not touch rt_get_stats' counters. */
+int rt_count_work(rt_ctx* ctx, int width, int height, rt_work* out_work);
 
 #ifdef __cplusplus
 } /* extern "C" */

@@ -53,10 +53,11 @@ def test_struct_layouts_match_header():
     assert C.sizeof(abi.rt_light) == 16
     assert C.sizeof(abi.rt_camera) == 20
     assert C.sizeof(abi.rt_stats) == 8 * 8 + 4 * 8 + 3 * 8
+    assert C.sizeof(abi.rt_work) == 8 * 8
 
 
 def test_abi_version(rtlib):
-    assert rtlib.rt_abi_version() == 4 == abi.RT_ABI_VERSION
+    assert rtlib.rt_abi_version() == 5 == abi.RT_ABI_VERSION
     hdr = open(HEADER).read()
     assert re.search(r"#define RT_ABI_VERSION (\d+)", hdr).group(1) == str(abi.RT_ABI_VERSION)
 
@@ -114,6 +115,8 @@ def test_null_arguments_are_errors(rtlib):
     assert rtlib.rt_set_scene(None, None, 0, None, 0, None, 0, abi.rt_vec3(0, 0, 0), 0) == abi.RT_ERR_INVALID_ARG
     assert rtlib.rt_render(None, 4, 4, None) == abi.RT_ERR_INVALID_ARG
     assert rtlib.rt_create(0, C.byref(C.c_void_p())) == abi.RT_ERR_INVALID_ARG
+    assert rtlib.rt_create_ex(1, 0x100, C.byref(C.c_void_p())) == abi.RT_ERR_INVALID_ARG  # unknown flag
+    assert rtlib.rt_count_work(None, 4, 4, None) == abi.RT_ERR_INVALID_ARG
     assert rtlib.rt_set_timing(None, 1) == abi.RT_ERR_INVALID_ARG
     assert rtlib.rt_debug_segments(None, 4, 4, 1, None, 0, C.byref(C.c_int())) == abi.RT_ERR_INVALID_ARG
 
@@ -182,7 +185,7 @@ def test_ctypes_layouts_match_the_c_header(tmp_path):
     ctypes mirror (what the C#/Go/Python bindings must reproduce)."""
     import subprocess
     structs = {n: getattr(abi, n) for n in ("rt_vec3", "rt_material", "rt_sphere", "rt_plane", "rt_light",
-                                           "rt_camera", "rt_view", "rt_segment", "rt_stats", "rt_wire_layout")}
+                                           "rt_camera", "rt_view", "rt_segment", "rt_stats", "rt_work", "rt_wire_layout")}
     lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "raytracer_hip.h"', "int main(void) {"]
     for n, t in structs.items():
         lines.append(f'printf("{n} %zu\\n", sizeof({n}));')

@@ -1,0 +1,61 @@
+"""bench.py's launcher and launch plan (CPU only): `--gpus N` without a torch.distributed
+launcher starts N ranks itself, every rank checks WORLD_SIZE == N, a box with fewer than N
+devices fails instead of silently running one GPU, and short runs split into balanced launches."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def test_plan_launches_balanced():
+    assert bench.plan_launches(20, 64) == [20]
+    assert bench.plan_launches(100, 64) == [50, 50]
+    assert bench.plan_launches(1024, 64) == [64] * 16
+    assert bench.plan_launches(65, 64) == [33, 32]
+    assert bench.plan_launches(0, 64) == []
+    for n in range(1, 300):
+        p = bench.plan_launches(n, 64)
+        assert sum(p) == n and max(p) <= 64 and max(p) - min(p) <= 1 and len(p) == -(-n // 64)
+
+
+def test_world_check():
+    a = bench.parse(["--gpus", "4"])
+    assert bench.world_check(a, {}) == ("spawn", "")
+    assert bench.world_check(a, {"WORLD_SIZE": "4"}) == ("run", "")
+    act, msg = bench.world_check(a, {"WORLD_SIZE": "2"})
+    assert act == "fail" and "WORLD_SIZE=2" in msg
+    assert bench.world_check(bench.parse([]), {}) == ("run", "")
+    assert bench.world_check(bench.parse(["--gpus", "1"]), {"WORLD_SIZE": "1"}) == ("run", "")
+
+
+def test_launch_command():
+    cmd = bench.launch_command(["--gpus", "8", "--steps", "20"], 8, 29555)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and "--nnodes=1" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert "--master-port=29555" in cmd
+    i = cmd.index(os.path.join(ROOT, "bench.py"))
+    assert cmd[i + 1:] == ["--gpus", "8", "--steps", "20"]
+
+
+def test_gpus_2_without_devices_fails_loudly():
+    """On a box with fewer devices than --gpus (here: none) bench.py exits non-zero with a message."""
+    env = dict(os.environ)
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "4"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    if "GPU(s) visible" not in r.stderr:
+        pytest.skip("devices visible")
+    assert r.returncode == 2 and "--gpus 2: only" in r.stderr
+    assert not r.stdout.strip()  # no bench line from a silent one-GPU run
+
+
+def test_rank_world_mismatch_fails():
+    env = dict(os.environ, WORLD_SIZE="3", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "WORLD_SIZE=3 but --gpus 2" in r.stderr

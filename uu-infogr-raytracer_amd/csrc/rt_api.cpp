@@ -93,6 +93,7 @@ struct Device {
     float tab_pw = 0, tab_ph = 0;
     int async_next = 0;
     unsigned long long* d_counters = nullptr;
+    unsigned long long* d_counters_diag = nullptr;  // rt_count_work
     std::vector<EventPair> pending, pool;
     uint64_t op_count[3] = {0, 0, 0};  // operations per timing kind (sampling phase)
     ncclComm_t comm = nullptr;
@@ -100,7 +101,7 @@ struct Device {
 
 struct SceneLayout {
     int S = 0, P = 0, L = 0, limit = 0;
-    size_t off_sph = 0, off_mat = 0, off_pl = 0, off_li = 0, off_cull = 0, off_shc = 0, bytes = 0;
+    size_t off_sph = 0, off_mat = 0, off_pl = 0, off_li = 0, off_cull = 0, bytes = 0;
     bool generic_pow = false;        // a specular material with n not in {0.5, 1, 2}
     std::vector<DevSphere> host_sph;  // for the per-frame primary constants
 };
@@ -108,6 +109,7 @@ struct SceneLayout {
 
 struct rt_ctx {
     int n_gpus = 1;
+    bool rccl_gather = false;  // rt_render through row bands + RCCL gather (n_gpus > 1 or RT_CREATE_RCCL_GATHER)
     std::vector<Device> dev;
     bool has_scene = false;
     SceneLayout layout;
@@ -327,7 +329,6 @@ void scene_params(const rt_ctx* ctx, const Device& d, LaunchParams& lp) {
     lp.pl = (const DevPlane*)(base + L.off_pl);
     lp.li = (const DevLight*)(base + L.off_li);
     lp.scull = (const DevSphereCull*)(base + L.off_cull);
-    lp.shc = (const DevShadowCull*)(base + L.off_shc);
     lp.S = L.S, lp.P = L.P, lp.L = L.L, lp.limit = L.limit;
     lp.counters = d.d_counters;
 }
@@ -380,7 +381,7 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
     hipStream_t saved = d.stream;
     d.stream = stream;
     const bool timed = begin_timed(ctx, d, 0);
-    int e = launch_trace(lp, ctx->layout.generic_pow, stream);
+    int e = launch_trace(lp, ctx->layout.generic_pow, false, stream);
     end_timed(d, timed);
     d.stream = saved;
     if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "trace launch failed: %s", hipGetErrorString((hipError_t)e));
@@ -423,8 +424,11 @@ const char* rt_last_error(const rt_ctx* ctx) {
     return g_last_error.c_str();
 }
 
-int rt_create(int n_gpus, rt_ctx** out_ctx) {
-    if (!out_ctx || n_gpus < 1) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_create: bad arguments");
+int rt_create(int n_gpus, rt_ctx** out_ctx) { return rt_create_ex(n_gpus, 0, out_ctx); }
+
+int rt_create_ex(int n_gpus, int flags, rt_ctx** out_ctx) {
+    if (!out_ctx || n_gpus < 1 || (flags & ~RT_CREATE_RCCL_GATHER) != 0)
+        return fail(nullptr, RT_ERR_INVALID_ARG, "rt_create: bad arguments");
     *out_ctx = nullptr;
     int ndev = 0;
     if (rt_device_count(&ndev) != RT_OK || ndev == 0)
@@ -433,12 +437,13 @@ int rt_create(int n_gpus, rt_ctx** out_ctx) {
     rt_ctx* ctx = new (std::nothrow) rt_ctx();
     if (!ctx) return fail(nullptr, RT_ERR_OOM, "out of host memory");
     ctx->n_gpus = n_gpus;
+    ctx->rccl_gather = n_gpus > 1 || (flags & RT_CREATE_RCCL_GATHER) != 0;
     ctx->dev.resize((size_t)n_gpus);
     int cur = 0;
     (void)hipGetDevice(&cur);
     for (int g = 0; g < n_gpus; ++g) {
         Device& d = ctx->dev[(size_t)g];
-        d.id = n_gpus == 1 ? cur : g;  // single-GPU: the caller's current device
+        d.id = n_gpus == 1 ? cur : g;  // one device: the caller's current one
         DeviceGuard guard(d.id);
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, d.id) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
@@ -458,7 +463,7 @@ int rt_create(int n_gpus, rt_ctx** out_ctx) {
             return rc;
         }
     }
-    if (n_gpus > 1) {
+    if (ctx->rccl_gather) {
         std::string err;
         if (!g_rccl.load(err)) {
             fail(ctx, RT_ERR_RCCL, "%s", err.c_str());
@@ -496,6 +501,7 @@ void rt_destroy(rt_ctx* ctx) {
         for (int i = 0; i < 2; ++i)
             if (d.d_frames2[i]) (void)hipFree(d.d_frames2[i]);
         if (d.d_counters) (void)hipFree(d.d_counters);
+        if (d.d_counters_diag) (void)hipFree(d.d_counters_diag);
         if (d.d_view_tab) (void)hipFree(d.d_view_tab);
         if (d.d_stage) (void)hipFree(d.d_stage);
         for (hipStream_t s : d.slot_stream)
@@ -526,8 +532,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
     L.off_pl = al(L.off_mat + sizeof(DevMaterial) * (size_t)(n_spheres + n_planes));
     L.off_li = al(L.off_pl + sizeof(DevPlane) * (size_t)n_planes);
     L.off_cull = al(L.off_li + sizeof(DevLight) * (size_t)n_lights);
-    L.off_shc = al(L.off_cull + sizeof(DevSphereCull) * (size_t)n_spheres);
-    L.bytes = al(L.off_shc + sizeof(DevShadowCull) * (size_t)n_spheres * (size_t)n_lights) + 256;
+    L.bytes = al(L.off_cull + sizeof(DevSphereCull) * (size_t)n_spheres) + 256;
 
     std::vector<unsigned char> blob(L.bytes, 0);
     DevSphere* sph = (DevSphere*)(blob.data() + L.off_sph);
@@ -535,7 +540,6 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
     DevPlane* pl = (DevPlane*)(blob.data() + L.off_pl);
     DevLight* li = (DevLight*)(blob.data() + L.off_li);
     DevSphereCull* cull = (DevSphereCull*)(blob.data() + L.off_cull);
-    DevShadowCull* shc = (DevShadowCull*)(blob.data() + L.off_shc);
     for (int i = 0; i < n_spheres; ++i) {
         const rt_sphere& s = spheres[i];
         sph[i] = DevSphere{s.center.x, s.center.y, s.center.z, s.radius * s.radius};  // :336
@@ -582,20 +586,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
         d.ax = (float)A[0], d.ay = (float)A[1], d.az = (float)A[2];
         d.ux = (float)U[0], d.uy = (float)U[1], d.uz = (float)U[2];
         d.vx = (float)V[0], d.vy = (float)V[1], d.vz = (float)V[2];
-        d.lane_cull = (d.a >= 0x1p-40f && d.a <= 0x1p40f && std::isfinite(d.a2)) ? 1u : 0u;
         li[i] = d;
-        // per-lane shadow cull records (see DevShadowCull): centre in the light's frame,
-        // threshold base rounded up; spheres outside the analysed range are never culled
-        for (int k = 0; k < n_spheres; ++k) {
-            const DevSphere& s = sph[k];
-            const double cn = std::fabs((double)s.cx) + std::fabs((double)s.cy) + std::fabs((double)s.cz);
-            const double cu = (double)s.cx * d.ux + (double)s.cy * d.uy + (double)s.cz * d.uz;
-            const double cv = (double)s.cx * d.vx + (double)s.cy * d.vy + (double)s.cz * d.vz;
-            float t0 = INFINITY;
-            if (cull[k].rr >= 0x1p-50f && cull[k].rr < 0x1p40f && cn < 0x1p40 && std::isfinite(cu) && std::isfinite(cv))
-                t0 = std::nextafter((float)((double)cull[k].rr + 0x1p-8 * cn * (1.0 + 0x1p-20)), INFINITY);
-            shc[(size_t)i * n_spheres + k] = DevShadowCull{(float)cu, (float)cv, t0, 0.0f};
-        }
     }
     for (int i = 0; i < n_spheres + n_planes; ++i)
         if ((mat[i].flags & MAT_SPEC) && mat[i].pow_kind == POW_GENERIC) L.generic_pow = true;
@@ -873,7 +864,7 @@ int rt_render(rt_ctx* ctx, int width, int height, int32_t* pixels) {
     if (!pixels) return fail(ctx, RT_ERR_INVALID_ARG, "NULL pixels");
     const size_t frame_bytes = (size_t)width * height * sizeof(int32_t);
     Device& d0 = ctx->dev[0];
-    if (ctx->n_gpus == 1) {
+    if (!ctx->rccl_gather) {
         DeviceGuard guard(d0.id);
         rc = grow(ctx, (void**)&d0.d_frame, &d0.frame_cap, frame_bytes);
         if (rc != RT_OK) return rc;
@@ -945,7 +936,7 @@ int rt_render_async(rt_ctx* ctx, int width, int height, int32_t* pixels) {
     int rc = check_ctx(ctx, width, height);
     if (rc != RT_OK) return rc;
     if (!pixels) return fail(ctx, RT_ERR_INVALID_ARG, "NULL pixels");
-    if (ctx->n_gpus != 1) return rt_render(ctx, width, height, pixels);
+    if (ctx->rccl_gather) return rt_render(ctx, width, height, pixels);
     Device& d = ctx->dev[0];
     DeviceGuard guard(d.id);
     const size_t frame_bytes = (size_t)width * height * sizeof(int32_t);
@@ -1049,13 +1040,13 @@ int rt_get_stats(rt_ctx* ctx, rt_stats* out) {
         HIP_TRY(ctx, hipMemcpy(h.data(), d.d_counters, COUNTER_WORDS * sizeof(unsigned long long),
                                hipMemcpyDeviceToHost));
         for (int slot = 0; slot < COUNTER_SLOTS; ++slot)
-            for (int i = 0; i < 4; ++i) c[i] += h[(size_t)slot * 4 + i];
+            for (int i = 0; i < 4; ++i) c[i] += h[(size_t)slot * COUNTER_STRIDE + i];
     }
     out->frames = ctx->frames;
     out->pixels = ctx->pixels;
     out->primary_rays = ctx->prim_rays;
-    out->reflect_rays = c[1];
-    out->shadow_rays = c[2];
+    out->reflect_rays = c[CNT_REFLECT];
+    out->shadow_rays = c[CNT_SHADOW];
     const uint64_t S = (uint64_t)ctx->layout.S, P = (uint64_t)ctx->layout.P;
     out->sphere_tests = (ctx->prim_rays + c[1] + c[2]) * S;
     out->plane_tests = (ctx->prim_rays + c[1]) * P;
@@ -1091,6 +1082,52 @@ int rt_reset_stats(rt_ctx* ctx) {
     ctx->kernel_ms = ctx->last_kernel_ms = ctx->copy_ms = ctx->gather_ms = 0;
     ctx->timed[0] = ctx->timed[1] = ctx->timed[2] = 0;
     for (Device& d : ctx->dev) d.op_count[0] = d.op_count[1] = d.op_count[2] = 0;
+    return RT_OK;
+}
+
+int rt_count_work(rt_ctx* ctx, int width, int height, rt_work* out) {
+    int rc = check_ctx(ctx, width, height);
+    if (rc != RT_OK) return rc;
+    if (!out) return fail(ctx, RT_ERR_INVALID_ARG, "rt_count_work: NULL out_work");
+    if (ctx->n_gpus != 1) return fail(ctx, RT_ERR_INVALID_ARG, "rt_count_work needs a single-GPU context");
+    Device& d = ctx->dev[0];
+    DeviceGuard guard(d.id);
+    LaunchParams lp;
+    std::memset(&lp, 0, sizeof lp);
+    rc = view_params(ctx, width, height, lp);
+    if (rc != RT_OK) return rc;
+    scene_params(ctx, d, lp);
+    rc = view_tables(ctx, d, lp);
+    if (rc != RT_OK) return rc;
+    rc = grow(ctx, (void**)&d.d_frame, &d.frame_cap, (size_t)width * height * sizeof(int32_t));
+    if (rc != RT_OK) return rc;
+    if (!d.d_counters_diag)
+        HIP_TRY(ctx, hipMalloc((void**)&d.d_counters_diag, COUNTER_WORDS * sizeof(unsigned long long)));
+    HIP_TRY(ctx, hipMemsetAsync(d.d_counters_diag, 0, COUNTER_WORDS * sizeof(unsigned long long), d.stream));
+    lp.counters = d.d_counters_diag;
+    lp.band_rows = height, lp.band_first = 0, lp.band_step = 1, lp.local_rows = height;
+    lp.out = d.d_frame;
+    lp.out_fmt = RT_BANDS_INT32;
+    lp.n_frames = 1;
+    int e = launch_trace(lp, ctx->layout.generic_pow, true, d.stream);
+    if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "rt_count_work launch: %s", hipGetErrorString((hipError_t)e));
+    std::vector<unsigned long long> h(COUNTER_WORDS);
+    HIP_TRY(ctx, hipMemcpyAsync(h.data(), d.d_counters_diag, COUNTER_WORDS * sizeof(unsigned long long),
+                                hipMemcpyDeviceToHost, d.stream));
+    HIP_TRY(ctx, hipStreamSynchronize(d.stream));
+    unsigned long long c[COUNTER_STRIDE] = {};
+    for (int slot = 0; slot < COUNTER_SLOTS; ++slot)
+        for (int i = 0; i < COUNTER_STRIDE; ++i) c[i] += h[(size_t)slot * COUNTER_STRIDE + i];
+    const uint64_t S = (uint64_t)ctx->layout.S, P = (uint64_t)ctx->layout.P;
+    std::memset(out, 0, sizeof *out);
+    out->primary_rays = (uint64_t)width * (uint64_t)height;
+    out->reflect_rays = c[CNT_REFLECT];
+    out->shadow_rays = c[CNT_SHADOW];
+    out->sphere_tests = (out->primary_rays + out->reflect_rays + out->shadow_rays) * S;
+    out->plane_tests = (out->primary_rays + out->reflect_rays) * P;
+    out->shadow_rays_run = c[CNT_SHADOW_RUN];
+    out->sphere_tests_run = c[CNT_SPHERE_RUN];
+    out->plane_tests_run = c[CNT_PLANE_RUN];
     return RT_OK;
 }
 

@@ -47,7 +47,7 @@ struct DevLight {
     float a;      // dot(p, p)       : IntersectsSphere's `a` for a shadow ray (dir = position)
     float a2;     // 2 * a
     float a4;     // 4 * a
-    uint32_t lane_cull;  // 1: the per-lane shadow cull may be used (a in [2^-40, 2^40], 2a finite)
+    uint32_t pad0;
     // shadow-cull frame (culling only, never in a result): A ~ p/|p| (every shadow ray of this
     // light has direction p), U, V ~ orthonormal to A
     float ax, ay, az, pad1;
@@ -60,19 +60,15 @@ struct DevSphereCull {
     float cx, cy, cz, rr;
 };
 
-// Per-(light, sphere) record of the direct kernel's per-lane shadow cull [L][S]: the
-// sphere centre in the light's frame (cu = C.U, cv = C.V) and the threshold base
-// t0 >= r' + 2^-8 |C|_1 (rounded up; +inf when the sphere may not be culled).  A shadow
-// ray from hp skips sphere i when (cu - hp.U)^2 + (cv - hp.V)^2 > (t0 + 2^-8 |hp|_1)^2
-// (culling only; rt_kernel.hip, shadow_lane_cull, for why this is exact).
-struct DevShadowCull {
-    float cu, cv, t0, pad;
-};
-
 // Work counters: each workgroup adds its totals into slot (block id % COUNTER_SLOTS) so that
-// the atomics of thousands of workgroups do not serialise on one address.
+// the atomics of thousands of workgroups do not serialise on one address.  Per slot:
+// reflected segments and shadow rays of the visible path (every launch), and the executed
+// work of the diagnostic kernels (rt_count_work): shadow rays whose sphere loop ran, exact
+// sphere and plane tests run.
 constexpr int COUNTER_SLOTS = 256;
-constexpr int COUNTER_WORDS = COUNTER_SLOTS * 4;
+constexpr int COUNTER_STRIDE = 8;
+constexpr int COUNTER_WORDS = COUNTER_SLOTS * COUNTER_STRIDE;
+enum : int { CNT_REFLECT = 1, CNT_SHADOW = 2, CNT_SHADOW_RUN = 3, CNT_SPHERE_RUN = 4, CNT_PLANE_RUN = 5 };
 
 // Camera-relative sphere constants of the primary segment (origin = camera position for
 // every pixel): oc = cam - center and c = Dot(oc, oc) - r^2 of IntersectsSphere
@@ -103,7 +99,6 @@ struct LaunchParams {
     const DevPlane* pl;
     const DevLight* li;
     const DevSphereCull* scull;  // [S]
-    const DevShadowCull* shc;    // [L][S]
     const float* lxt;  // [W]: ((float)x / W - 0.5f) * pw, TracePixel :963-965
     const float* lyt;  // [H]: ((float)y / H - 0.5f) * ph
     int S, P, L, limit;
@@ -118,7 +113,7 @@ struct LaunchParams {
     int32_t* out;
     unsigned long long out_frame_bytes;  // batch launches: frame z of the grid at (char*)out + z * out_frame_bytes
     int out_fmt;  // 0: int32 0x00RRGGBB per pixel; 1: packed 24-bit (bytes B, G, R); 2: int32 at frame row y
-    unsigned long long* counters;  // COUNTER_SLOTS x {primary, reflect, shadow, pad}
+    unsigned long long* counters;  // COUNTER_SLOTS x COUNTER_STRIDE (CNT_*)
     int prim_const;                // 1: pc[0..S) and pbox[0..S) valid (S <= MAX_PRIM_CONST)
     PrimConst pc[MAX_PRIM_CONST];
     PrimBox pbox[MAX_PRIM_CONST];
@@ -134,7 +129,8 @@ struct DevSegment {
 int launch_debug_segments(const LaunchParams& p, int stride, DevSegment* out, int capacity, unsigned* count,
                           void* stream);
 // generic_pow: some material needs the f64 Math.Pow path (exponent not 0.5, 1 or 2).
-int launch_trace(const LaunchParams& p, bool generic_pow, void* stream);
+// stats: the diagnostic kernels that also tally the executed work (CNT_*_RUN).
+int launch_trace(const LaunchParams& p, bool generic_pow, bool stats, void* stream);
 // All ranks' gathered band sets (rank r's at g + r * slot_bytes, format fmt) -> frame.
 int launch_scatter_gathered(const unsigned char* g, size_t slot_bytes, int fmt, int32_t* frame, int W, int H,
                             int band_rows, int world, void* stream);

@@ -33,28 +33,9 @@
 #define RT_FASTMATH 1
 #endif
 
-// RT_ABLATE (timing experiments only, tools/ab.py; never defined in the shipped build):
-//   1 = no shading (fold skipped), 2 = no shadow rays, 3 = primary segment only.
-#ifndef RT_ABLATE
-#define RT_ABLATE 0
-#endif
-// RT_CULLSTATS (experiments only): the bundle kernel's reflect/shadow counters count the
-// wave-iterations of its shadow exact-test loops (1) or its shadow bundles (2) instead of rays.
-// Workgroup shape of the trace kernels: WG_WX x WG_WY waves, each an 8x8 pixel tile.
-// A/B (C2/C3/C4): 1x1 1.00/1.00/0.92, 2x1 0.99/1.00/0.95, 2x2 = 1, 4x2 1.04/1.03/1.13,
-// 4x4 1.10/1.14/1.29 (kernel time relative to 2x2).
-#ifndef RT_WG_WX
-#define RT_WG_WX 1
-#endif
-#ifndef RT_WG_WY
-#define RT_WG_WY 1
-#endif
-constexpr int WG_WX = RT_WG_WX, WG_WY = RT_WG_WY, WG_WAVES = WG_WX * WG_WY, WG_THREADS = 64 * WG_WAVES;
-[[maybe_unused]] constexpr int TILE_W = 8 * WG_WX, TILE_H = 8 * WG_WY;
-
-#ifndef RT_CULLSTATS
-#define RT_CULLSTATS 0
-#endif
+// One wave (64 lanes, an 8x8 pixel tile) per workgroup: a one-wave group releases its LDS
+// stack slots as soon as it ends (A/B round 1: 2x2-wave groups +8 % on C4).
+constexpr int WG_THREADS = 64, TILE_W = 8, TILE_H = 8;
 
 namespace rtk {
 
@@ -240,98 +221,24 @@ __device__ __forceinline__ void store_pixel(const LaunchParams& p, int r, int y,
     }
 }
 
-// Per-lane level stack.  Records: a = {hit point, t}, b = {incoming direction, primitive code}.
-template <int K, bool SCRATCH>
-struct LevelStack;
-
-// Register stack: K fixed, static indices only (shift on push/pop) so it stays in VGPRs.
+// Deep-recursion stack (recursion limits >= 8): whole records {hit point, t} and {incoming
+// direction, primitive code}, dynamically indexed, in scratch.
 template <int K>
-struct LevelStack<K, false> {
+struct ScratchStack {
     float4 a[K], b[K];
     int n = 0;
-    __device__ __forceinline__ void push(float4 x, float4 y) {
-#pragma unroll
-        for (int i = K - 1; i > 0; --i) {
-            a[i] = a[i - 1];
-            b[i] = b[i - 1];
-        }
-        a[0] = x;
-        b[0] = y;
-        ++n;
-    }
-    __device__ __forceinline__ void pop(float4& x, float4& y) {
-        x = a[0];
-        y = b[0];
-#pragma unroll
-        for (int i = 0; i < K - 1; ++i) {
-            a[i] = a[i + 1];
-            b[i] = b[i + 1];
-        }
-        --n;
-    }
-};
-
-// Deep-recursion stack (recursion limits >= 8): dynamically indexed, lives in scratch.
-template <int K>
-struct LevelStack<K, true> {
-    float4 a[K], b[K];
-    int n = 0;
+    __device__ __forceinline__ ScratchStack(float2*, float*) {}
+    __device__ __forceinline__ void origin(f3) {}
     __device__ __forceinline__ void push(float4 x, float4 y) {
         a[n] = x;
         b[n] = y;
         ++n;
     }
-    __device__ __forceinline__ void pop(float4& x, float4& y) {
+    __device__ __forceinline__ void pop(const LaunchParams&, float4& x, float4& y) {
         --n;
         x = a[n];
         y = b[n];
     }
-};
-
-// Hybrid stack for limits 3..7: the two most recent records in VGPRs, older ones in a
-// per-lane scratch array (touched only by lanes more than two levels deep -- rare), so the
-// kernel keeps its occupancy: 16 VGPRs instead of 8 x K.
-template <int K>
-struct HybridOverflow {
-    float4 a[K - 2], b[K - 2];  // older records (dynamically indexed: scratch)
-};
-template <int K>
-struct HybridStack {
-    float4 a0, b0, a1, b1;  // top record, second record (separate SSA values: VGPRs)
-    HybridOverflow<K>* ov;  // a separate object, so only it is demoted to scratch
-    int n = 0;
-    __device__ __forceinline__ HybridStack(HybridOverflow<K>* o, float2*, float*) : ov(o) {}
-    __device__ __forceinline__ void push(float4 x, float4 y) {
-        if (n >= 2) {  // spill the second record
-            ov->a[n - 2] = a1;
-            ov->b[n - 2] = b1;
-        }
-        a1 = a0;
-        b1 = b0;
-        a0 = x;
-        b0 = y;
-        ++n;
-    }
-    __device__ __forceinline__ void origin(f3) {}
-    __device__ __forceinline__ void pop(const LaunchParams&, float4& x, float4& y) {
-        x = a0;
-        y = b0;
-        a0 = a1;
-        b0 = b1;
-        --n;
-        if (n >= 2) {  // refill the second record
-            a1 = ov->a[n - 2];
-            b1 = ov->b[n - 2];
-        }
-    }
-};
-
-struct NoOverflow {};
-template <int K, bool SCRATCH>
-struct PlainStack : LevelStack<K, SCRATCH> {
-    __device__ __forceinline__ PlainStack(NoOverflow*, float2*, float*) {}
-    __device__ __forceinline__ void origin(f3) {}
-    __device__ __forceinline__ void pop(const LaunchParams&, float4& x, float4& y) { LevelStack<K, SCRATCH>::pop(x, y); }
 };
 
 // One reflection step of the forward walk (TraceSphere :854 / TracePlane normal,
@@ -352,113 +259,17 @@ __device__ __forceinline__ f3 reflect_at(const LaunchParams& p, f3 o, f3& d, flo
     return hp;
 }
 
-// Compact stacks: a record is fully determined by the camera ray and the (t, primitive)
-// pairs of the levels above it, so older levels keep only those 8 bytes (registers,
-// statically indexed) and are rebuilt by re-walking the reflection chain -- no scratch
-// traffic at all.
-// RT_STACK 1: every level compact, each pop re-walks (level k costs k steps).  The levels
-// live in register vectors; the re-walk loop is rolled with a wave-uniform index (indirect
-// register reads, no scratch), the per-lane top is picked by a select chain.
-template <int K>
-struct CompactStack {
-    typedef float tvec __attribute__((ext_vector_type(K)));
-    typedef int cvec __attribute__((ext_vector_type(K)));
-    tvec t;
-    cvec c;
-    f3 d0;
-    int n = 0;
-    __device__ __forceinline__ CompactStack(NoOverflow*, float2*, float*) {}
-    __device__ __forceinline__ void origin(f3 d) { d0 = d; }
-    __device__ __forceinline__ void push(float4 x, float4 y) {
-#pragma unroll
-        for (int i = 0; i < K; ++i)
-            if (i == n) {
-                t[i] = x.w;
-                c[i] = __float_as_int(y.w);
-            }
-        ++n;
-    }
-    __device__ __forceinline__ void pop(const LaunchParams& p, float4& x, float4& y) {
-        --n;
-        f3 o = mk(p.cam[0], p.cam[1], p.cam[2]), d = d0;
-#pragma unroll 1
-        for (int j = 0; j < K - 1; ++j) {
-            const bool go = j < n;
-            if (__builtin_amdgcn_ballot_w64(go) == 0) break;
-            if (go) o = reflect_at(p, o, d, t[j], c[j]);
-        }
-        float tk = t[0];
-        int ck = c[0];
-#pragma unroll
-        for (int i = 1; i < K; ++i)
-            if (i == n) {
-                tk = t[i];
-                ck = c[i];
-            }
-        const f3 hp = add(o, scale(d, tk));
-        x = make_float4(hp.x, hp.y, hp.z, tk);
-        y = make_float4(d.x, d.y, d.z, __int_as_float(ck));
-    }
-};
-
-// RT_STACK 2: the two most recent records whole in VGPRs, older levels compact; only the
-// refill of the second record re-walks (levels n-3.. of an n-deep chain).
-template <int K>
-struct CompactHybridStack {
-    float4 a0, b0, a1, b1;
-    float t[K - 2];
-    int c[K - 2];
-    f3 d0;
-    int n = 0;
-    __device__ __forceinline__ CompactHybridStack(NoOverflow*, float2*, float*) {}
-    __device__ __forceinline__ void origin(f3 d) { d0 = d; }
-    __device__ __forceinline__ void push(float4 x, float4 y) {
-        if (n >= 2) {
-#pragma unroll
-            for (int i = 0; i < K - 2; ++i)
-                if (i == n - 2) {
-                    t[i] = a1.w;
-                    c[i] = __float_as_int(b1.w);
-                }
-        }
-        a1 = a0;
-        b1 = b0;
-        a0 = x;
-        b0 = y;
-        ++n;
-    }
-    __device__ __forceinline__ void pop(const LaunchParams& p, float4& x, float4& y) {
-        x = a0;
-        y = b0;
-        a0 = a1;
-        b0 = b1;
-        --n;
-        if (n >= 2) {  // rebuild level n-2 from the compact levels 0..n-2
-            f3 o = mk(p.cam[0], p.cam[1], p.cam[2]), d = d0;
-            float tk = t[0];
-            int ck = c[0];
-#pragma unroll
-            for (int j = 0; j < K - 3; ++j)
-                if (j < n - 2) {
-                    o = reflect_at(p, o, d, t[j], c[j]);
-                    tk = t[j + 1];
-                    ck = c[j + 1];
-                }
-            const f3 hp = add(o, scale(d, tk));
-            a1 = make_float4(hp.x, hp.y, hp.z, tk);
-            b1 = make_float4(d.x, d.y, d.z, __int_as_float(ck));
-        }
-    }
-};
-
-// RT_STACK 3: the compact levels and the primary direction in LDS, one slot per thread
+// Compact levels: a record is fully determined by the camera ray and the (t, primitive)
+// pairs of the levels above it, so each level keeps only those 8 bytes and pop rebuilds the
+// record by re-walking the reflection chain with reflect_at (bit-identical).
+// Level stack for limits 0..7: the compact levels and the primary direction in LDS, one slot per thread
 // ([level][thread], conflict-free), so they cost no VGPRs; pop re-walks as in CompactStack.
 template <int K>
 struct LdsStack {
     float2* lv;  // [K][WG_THREADS] (t, primitive code) of this workgroup
     float* dv;   // [3][WG_THREADS] primary direction
     int n = 0;
-    __device__ __forceinline__ LdsStack(NoOverflow*, float2* l, float* dd) : lv(l), dv(dd) {}
+    __device__ __forceinline__ LdsStack(float2* l, float* dd) : lv(l), dv(dd) {}
     __device__ __forceinline__ void origin(f3 d) {
         dv[threadIdx.x] = d.x;
         dv[WG_THREADS + threadIdx.x] = d.y;
@@ -488,52 +299,25 @@ struct LdsStack {
     }
 };
 
-#ifndef RT_STACK
-#define RT_STACK 3
-#endif
+// Stack type per K (= recursion limit + 1 records): the LDS stack up to 8 levels (A/B round 1:
+// no VGPRs for records, -2..-5.5 % on C4/C5 against register and hybrid stacks), scratch beyond.
 template <int K>
-struct MidStack {  // stack for K = 4, 6, 8
-#if RT_STACK == 3
-    using type = LdsStack<K>;
-    using overflow = NoOverflow;
-    static constexpr int lds_levels = K;
-#elif RT_STACK == 1
-    using type = CompactStack<K>;
-    using overflow = NoOverflow;
-    static constexpr int lds_levels = 0;
-#elif RT_STACK == 2
-    using type = CompactHybridStack<K>;
-    using overflow = NoOverflow;
-    static constexpr int lds_levels = 0;
-#else
-    using type = HybridStack<K>;
-    using overflow = HybridOverflow<K>;
-    static constexpr int lds_levels = 0;
-#endif
-};
-
-// Stack type per K: registers up to 2 records, MidStack up to 8, scratch beyond.
-template <int K, bool SCRATCH>
 struct StackFor {
-    using type = PlainStack<K, SCRATCH>;
-    using overflow = NoOverflow;
+    using type = ScratchStack<K>;
     static constexpr int lds_levels = 0;
 };
-#ifndef RT_LDS_SMALL
-#define RT_LDS_SMALL 1
-#endif
-#if RT_STACK == 3 && RT_LDS_SMALL
-template <>
-struct StackFor<1, false> : MidStack<1> {};
-template <>
-struct StackFor<2, false> : MidStack<2> {};
-#endif
-template <>
-struct StackFor<4, false> : MidStack<4> {};
-template <>
-struct StackFor<6, false> : MidStack<6> {};
-template <>
-struct StackFor<8, false> : MidStack<8> {};
+#define RT_LDS_STACK(K)                        \
+    template <>                                \
+    struct StackFor<K> {                       \
+        using type = LdsStack<K>;              \
+        static constexpr int lds_levels = K;   \
+    };
+RT_LDS_STACK(1)
+RT_LDS_STACK(2)
+RT_LDS_STACK(4)
+RT_LDS_STACK(6)
+RT_LDS_STACK(8)
+#undef RT_LDS_STACK
 
 // Sum of v over the wave (all lanes active): bit-sliced ballots and scalar popcounts, no
 // LDS round trips; the loop runs once per significant bit of the largest v (uniform).
@@ -544,62 +328,60 @@ __device__ __forceinline__ unsigned wave_count(unsigned v) {
     return s;
 }
 
-#ifndef RT_COUNTERS
-#define RT_COUNTERS 2
-#endif
 // Per-lane work counts share one register: reflected segments (<= RT_MAX_RECURSION_LIMIT + 1)
 // in the low byte, shadow rays (<= lights x 64; rt_set_scene caps lights at 65536) above.
 constexpr unsigned CNT_SHADOW_SHIFT = 8;
 constexpr unsigned CNT_REFL_MASK = 0xFFu;
-// Work counters of one wave (converged call, every lane of the workgroup reaches it):
-// RT_COUNTERS 1 = shuffle sums -> LDS -> one workgroup total per spread slot;
-// 2 = ballot/popcount sums, lane 0 adds the wave's reflect/shadow totals to slot
-// (wave id % 256); primary rays are the traced pixels, counted on the host.
-__device__ __forceinline__ unsigned wave_sum(unsigned v);
-__device__ __forceinline__ void add_counters(const LaunchParams& p, int lane, int wave, unsigned n_prim,
-                                             unsigned n_refl, unsigned n_shadow) {
-#if RT_COUNTERS == 1
-    __shared__ unsigned red[WG_WAVES][3];
-    n_prim = wave_sum(n_prim);
-    n_refl = wave_sum(n_refl);
-    n_shadow = wave_sum(n_shadow);
-    if (lane == 0) {
-        red[wave][0] = n_prim;
-        red[wave][1] = n_refl;
-        red[wave][2] = n_shadow;
-    }
-    __syncthreads();
-    if (threadIdx.x < 3) {
-        unsigned v = 0;
-        for (int w = 0; w < WG_WAVES; ++w) v += red[w][threadIdx.x];
-        const unsigned slot = (blockIdx.y * gridDim.x + blockIdx.x) % COUNTER_SLOTS;
-        if (v) atomicAdd(&p.counters[slot * 4 + threadIdx.x], (unsigned long long)v);
-    }
-#elif RT_COUNTERS == 2
-    // primary rays = traced pixels, counted on the host (every atomic is a memory round trip
-    // on MI355X: 32 B of HBM write traffic each)
-    (void)n_prim;
-    const unsigned b = wave_count(n_refl), c = wave_count(n_shadow);
-    if (lane == 0) {
-        const unsigned slot = ((blockIdx.y * gridDim.x + blockIdx.x) * (unsigned)WG_WAVES + (unsigned)wave) % COUNTER_SLOTS;
-        unsigned long long* q = &p.counters[slot * 4];
-        if (b) atomicAdd(q + 1, (unsigned long long)b);
-        if (c) atomicAdd(q + 2, (unsigned long long)c);
-    }
-#else
-    (void)p, (void)lane, (void)wave, (void)n_prim, (void)n_refl, (void)n_shadow;
-#endif
-}
 
-__device__ __forceinline__ unsigned wave_sum(unsigned v) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
+// Executed-work tally of the diagnostic kernels (STATS = true; never the timed ones): exact
+// IntersectsSphere / IntersectPlane evaluations a lane actually ran, and the shadow rays whose
+// sphere loop ran (a shadow ray is skipped when its outcome cannot change the pixel, and culling
+// skips sphere tests that provably cannot select) -- reported beside the nominal counts of
+// SURVEY.md 8(d), which count every primitive of every ray.
+template <bool ON>
+struct Tally {
+    __device__ __forceinline__ void sphere(bool) {}
+    __device__ __forceinline__ void plane(bool) {}
+    __device__ __forceinline__ void shadow(bool) {}
+};
+template <>
+struct Tally<true> {
+    unsigned s = 0, pl = 0, sh = 0;
+    __device__ __forceinline__ void sphere(bool c) { s += c ? 1u : 0u; }
+    __device__ __forceinline__ void plane(bool c) { pl += c ? 1u : 0u; }
+    __device__ __forceinline__ void shadow(bool c) { sh += c ? 1u : 0u; }
+};
+
+// Work counters of one wave (converged call): ballot/popcount sums, lane 0 adds the wave's
+// totals to slot (wave id % COUNTER_SLOTS); primary rays are the traced pixels, counted on the
+// host.  Every frame of a batch launch (grid z) traces the same view with the same
+// LaunchParams, so its counts are identical: frame 0 counts for all n_frames of them -- one
+// atomic pair per wave per launch instead of per frame (each device-scope atomic is a memory
+// round trip on MI355X, 32 B of HBM write traffic).
+template <bool ST>
+__device__ __forceinline__ void add_counters(const LaunchParams& p, int lane, unsigned n_refl, unsigned n_shadow,
+                                             const Tally<ST>& tl) {
+    if (blockIdx.z != 0) return;  // wave-uniform
+    const unsigned long long nf = p.n_frames > 1 ? (unsigned long long)p.n_frames : 1ull;
+    const unsigned b = wave_count(n_refl), c = wave_count(n_shadow);
+    const unsigned slot = (blockIdx.y * gridDim.x + blockIdx.x) % COUNTER_SLOTS;
+    unsigned long long* q = &p.counters[slot * COUNTER_STRIDE];
+    if (lane == 0) {
+        if (b) atomicAdd(q + CNT_REFLECT, b * nf);
+        if (c) atomicAdd(q + CNT_SHADOW, c * nf);
+    }
+    if constexpr (ST) {
+        const unsigned s = wave_count(tl.s), pl = wave_count(tl.pl), sh = wave_count(tl.sh);
+        if (lane == 0) {
+            if (sh) atomicAdd(q + CNT_SHADOW_RUN, sh * nf);
+            if (s) atomicAdd(q + CNT_SPHERE_RUN, s * nf);
+            if (pl) atomicAdd(q + CNT_PLANE_RUN, pl * nf);
+        }
+    }
 }
 
 // Sphere loop of the direct path: a runtime loop (SMAX = 0, shipped) or fully unrolled over
-// SMAX with uniform `i < S` guards.  In-process A/B of SMAX = 8: C2 +2.7 %, C3 -3.3 % -- not
-// taken.
+// SMAX with uniform `i < S` guards.
 template <int SMAX, typename F>
 __device__ __forceinline__ void for_spheres(int S, F&& f) {
     if constexpr (SMAX > 0) {
@@ -627,7 +409,7 @@ constexpr int HIT_NONE = 0x7fffffff;
 // every phong component is +-0 or NaN and I * att is finite, both give +-0 / NaN per
 // component (the sign of a zero never reaches a pixel: only additions, products, IEEE max and
 // the final clamp follow), so the test is skipped (RT_SHADOW_SKIP).  Ray counters are unchanged
-// (shadow rays = shaded diffuse hits x lights).
+// (shadow rays = shaded diffuse hits x lights); the diagnostic tally counts the tests that ran.
 #ifndef RT_SHADOW_SKIP
 #define RT_SHADOW_SKIP 1
 #endif
@@ -639,44 +421,9 @@ __device__ __forceinline__ bool shadow_matters(f3 ph, float intensity, float att
     return !(finite && zero_or_nan(ph.x) && zero_or_nan(ph.y) && zero_or_nan(ph.z));
 }
 
-// Per-lane shadow cull of the direct kernel (RT_LANE_SHADOW_CULL).  Every shadow ray of light
-// l has direction p_l (Q2), so sphere i can block the ray from hp only if the line
-// {hp + s p_l} passes within r of its centre C: in the light's host-built frame (U, V ~ unit,
-// orthogonal to A ~ p_l/|p_l|) that distance is D = |((C - hp).U, (C - hp).V)|.  The host
-// stores cu = C.U, cv = C.V and t0 >= r' + 2^-8 |C|_1 (r' >= r (1 + 2^-8)); the lane skips
-// the exact test when (cu - hp.U)^2 + (cv - hp.V)^2 > (t0 + 2^-8 |hp|_1)^2.
-// Exactness: with u = hp - C and N = |C|_1 + |hp|_1 >= |u|, the binary32 discriminant of
-// IntersectsSphere is negative whenever D >= r (1 + 3 eps) + 9.2e-4 |u| (the error analysis
-// of cull_mask, invariant in the scale of the direction; a in [2^-40, 2^40], |u| < 2^41, so
-// nothing overflows and, since a culled sphere has D > t0 >= 2^-25, nothing underflows),
-// and disc < 0 makes shadow_blocked false in both of its branches.  The rounding of the
-// cull arithmetic (cu, cv rounded from binary64, hp.U and hp.V in binary32, the frame's own
-// rounding) perturbs D by less than 2^-20 N, so a cull implies D > r (1 + 2^-8) + 2^-9 N,
-// twice the 9.2e-4 |u| needed.  NaN / inf anywhere, |hp|_1 >= 2^40, or a sphere the host
-// excluded (t0 = +inf) fail the comparison: the exact test runs.
-#ifndef RT_LANE_SHADOW_CULL
-#define RT_LANE_SHADOW_CULL 0
-#endif
-struct LaneShadowCull {
-    float hu, hv, m;
-};
-__device__ __forceinline__ LaneShadowCull lane_shadow_frame(f3 hp, const DevLight& l) {
-    LaneShadowCull c;
-    c.hu = dot(hp, mk(l.ux, l.uy, l.uz));
-    c.hv = dot(hp, mk(l.vx, l.vy, l.vz));
-    const float hn = __builtin_fabsf(hp.x) + __builtin_fabsf(hp.y) + __builtin_fabsf(hp.z);
-    c.m = hn < 0x1p40f ? hn * 0x1.004p-8f : __builtin_inff();  // >= 2^-8 |hp|_1
-    return c;
-}
-__device__ __forceinline__ bool lane_shadow_far(const LaneShadowCull& c, const DevShadowCull& s) {
-    const float du = s.cu - c.hu, dv = s.cv - c.hv;
-    const float t = s.t0 + c.m;
-    return __builtin_fmaf(du, du, dv * dv) > t * t;
-}
-
-template <bool GPOW, int SMAX>
+template <bool GPOW, int SMAX, typename T>
 __device__ __forceinline__ f3 shade_direct(const LaunchParams& p, bool is_sphere, int prim, f3 hp, f3 d, float t, f3 sec,
-                                    unsigned* n_shadow) {
+                                           unsigned* n_shadow, T& tl) {
     const DevMaterial& m = p.mat[is_sphere ? prim : p.S + prim];
     const uint32_t flags = m.flags;
     f3 normal;
@@ -714,19 +461,19 @@ __device__ __forceinline__ f3 shade_direct(const LaunchParams& p, bool is_sphere
             ph = add(ph, spec);
             bool blocked = false;
             if (shadow_matters(ph, l.intensity, att)) {
-                if constexpr (RT_ABLATE == 2) {
-                    blocked = hp.x > 1e30f;
-                } else if constexpr (SMAX > 0) {
+                tl.shadow(true);
+                if constexpr (SMAX > 0) {
                     for_spheres<SMAX>(p.S, [&](int i) {
-                        if (!blocked) blocked = shadow_blocked(hp, l, l_ok, p.sph[i]);
+                        if (!blocked) {
+                            tl.sphere(true);
+                            blocked = shadow_blocked(hp, l, l_ok, p.sph[i]);
+                        }
                     });
-                } else if (RT_LANE_SHADOW_CULL && l.lane_cull) {  // wave-uniform
-                    const LaneShadowCull c = lane_shadow_frame(hp, l);
-                    const DevShadowCull* sc = p.shc + li * p.S;
-                    for (int i = 0; i < p.S && !blocked; ++i)
-                        if (!lane_shadow_far(c, sc[i])) blocked = shadow_blocked(hp, l, l_ok, p.sph[i]);
                 } else {
-                    for (int i = 0; i < p.S && !blocked; ++i) blocked = shadow_blocked(hp, l, l_ok, p.sph[i]);
+                    for (int i = 0; i < p.S && !blocked; ++i) {
+                        tl.sphere(true);
+                        blocked = shadow_blocked(hp, l, l_ok, p.sph[i]);
+                    }
                 }
             }
             const float inten = blocked ? 0.0f : l.intensity;
@@ -745,36 +492,26 @@ __device__ __forceinline__ f3 shade_direct(const LaunchParams& p, bool is_sphere
 
 // Candidate spheres of a wave's primary rays: those whose per-frame screen box (view_params)
 // overlaps the wave's pixels.  Lanes 0 and 63 hold the wave's first and last pixel (the row
-// mapping is monotonic).  Converged call; p.prim_const required.
+// mapping is monotonic).  The wave's start has no dependent chain of memory round trips: the
+// box is one unconditional 16-byte load (lane 0's for lanes >= S), tested without
+// short-circuit branches.  Converged call; p.prim_const required.
 #ifndef RT_PRIM_BOX
 #define RT_PRIM_BOX 1
-#endif
-// RT_FAST_PROLOGUE (shipped): the wave's start has no dependent chain of memory round trips --
-// the box is one unconditional 16-byte load (lane 0's for lanes >= S), tested without
-// short-circuit branches, and the view-table loads are issued before it (tile_prologue).
-#ifndef RT_FAST_PROLOGUE
-#define RT_FAST_PROLOGUE 1
 #endif
 __device__ __forceinline__ unsigned long long prim_box_mask(const LaunchParams& p, int x, int y) {
     const int x_lo = __builtin_amdgcn_readlane(x, 0), x_hi = __builtin_amdgcn_readlane(x, 63);
     const int y_lo = __builtin_amdgcn_readlane(y, 0), y_hi = __builtin_amdgcn_readlane(y, 63);
     const int lane = threadIdx.x & 63;
-    bool cand = false;
-    if constexpr (RT_FAST_PROLOGUE) {
-        const bool in = lane < p.S;
-        const PrimBox b = p.pbox[in ? lane : 0];
-        cand = in & (b.x0 <= x_hi) & (b.x1 >= x_lo) & (b.y0 <= y_hi) & (b.y1 >= y_lo);
-    } else if (lane < p.S) {
-        const PrimBox b = p.pbox[lane];
-        cand = b.x0 <= x_hi && b.x1 >= x_lo && b.y0 <= y_hi && b.y1 >= y_lo;
-    }
+    const bool in = lane < p.S;
+    const PrimBox b = p.pbox[in ? lane : 0];
+    const bool cand = in & (b.x0 <= x_hi) & (b.x1 >= x_lo) & (b.y0 <= y_hi) & (b.y1 >= y_lo);
     return __builtin_amdgcn_ballot_w64(cand);
 }
 
 // A wave's pixels: column x, local row r -> frame row y (band band_first + (r / band_rows) *
 // band_step), validity, and the view-table entries lx = lxt[x], ly = lyt[y] (0 outside).
 // Fast paths without a per-lane integer division: one band (every full-frame launch) and the
-// 8-row bands of the multi-GPU path.
+// 8-row bands of the multi-GPU path; the view-table loads are unconditional.
 struct TilePixel {
     int x, r, y;
     bool valid;
@@ -783,9 +520,9 @@ struct TilePixel {
 __device__ __forceinline__ TilePixel tile_pixel(const LaunchParams& p, int x, int r) {
     TilePixel t;
     t.x = x, t.r = r;
-    if (RT_FAST_PROLOGUE && p.band_rows >= p.local_rows) {  // wave-uniform branches
+    if (p.band_rows >= p.local_rows) {  // wave-uniform branches
         t.y = p.band_first * p.band_rows + r;
-    } else if (RT_FAST_PROLOGUE && p.band_rows == 8) {
+    } else if (p.band_rows == 8) {
         t.y = (p.band_first + (r >> 3) * p.band_step) * 8 + (r & 7);
     } else {
         const int band = p.band_first + (r / p.band_rows) * p.band_step;
@@ -797,8 +534,8 @@ __device__ __forceinline__ TilePixel tile_pixel(const LaunchParams& p, int x, in
     return t;
 }
 
-template <bool PRIMARY, int SMAX>
-__device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d, unsigned long long pmask = 0) {
+template <bool PRIMARY, int SMAX, typename T>
+__device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d, T& tl, unsigned long long pmask = 0) {
     const float a = dot(d, d);
     const float a2 = 2.0f * a, a4 = 4.0f * a;
     const bool a2_ok = a2 > 0.0f && a2 < __builtin_inff();
@@ -807,6 +544,7 @@ __device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d,
     if (PRIMARY && p.prim_const) {
         // o == camera: oc = cam - c and c = oc.oc - r^2 are the same per frame (:614-619)
         auto test = [&](int i) {
+            tl.sphere(true);
             const PrimConst pc = p.pc[i];
             const float b = 2.0f * dot(mk(pc.ocx, pc.ocy, pc.ocz), d);
             const float disc = b * b - a4 * pc.c;
@@ -824,6 +562,7 @@ __device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d,
         }
     } else {
         for_spheres<SMAX>(p.S, [&](int i) {
+            tl.sphere(true);
             const float t = sphere_t(o, d, a2, a4, a2_ok, p.sph[i]);
             if (PRIMARY) {
                 if (t > 0.0f && best_s > t) {
@@ -842,6 +581,7 @@ __device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d,
     float best_p = __builtin_inff();
     int win_p = -1;
     for (int i = 0; i < p.P; ++i) {
+        tl.plane(true);
         const float t = plane_t(o, d, p.pl[i]);
         if (t > 0.0f && t < best_p) {
             best_p = t;
@@ -862,11 +602,12 @@ __device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d,
 #ifndef RT_TERMINAL
 #define RT_TERMINAL 1
 #endif
-template <int SMAX>
-__device__ __forceinline__ Hit terminal_direct(const LaunchParams& p, f3 o, f3 d) {
+template <int SMAX, typename T>
+__device__ __forceinline__ Hit terminal_direct(const LaunchParams& p, f3 o, f3 d, T& tl) {
     float best_p = __builtin_inff();
     int win_p = -1;
     for (int i = 0; i < p.P; ++i) {
+        tl.plane(true);
         const float t = plane_t(o, d, p.pl[i]);
         if (t > 0.0f && t < best_p) {
             best_p = t;
@@ -879,6 +620,7 @@ __device__ __forceinline__ Hit terminal_direct(const LaunchParams& p, f3 o, f3 d
     const bool a2_ok = a2 > 0.0f && a2 < __builtin_inff();
     float best_s = __builtin_inff();
     for_spheres<SMAX>(p.S, [&](int i) {
+        tl.sphere(true);
         const float t = sphere_t(o, d, a2, a4, a2_ok, p.sph[i]);
         const float tm = t - 0.01f;
         if (tm > 0.0f && tm < best_s) best_s = t;
@@ -888,28 +630,19 @@ __device__ __forceinline__ Hit terminal_direct(const LaunchParams& p, f3 o, f3 d
 }
 
 // DIRECT kernel: each lane walks its own chain with per-lane (divergent) control flow.
-template <int K, bool SCRATCH, bool GPOW, int SMAX>
-// RT_PRIO (experiment): issue priority by phase.  > 0 raises it as a wave reaches its later
-// phases (1: for the backward fold; 2: 1 after the primary segment, 2 for the fold) -- older
-// waves win VALU arbitration even more than by age (C2 +15 %, C3 +9…17 %: rejected).  < 0 gives
-// young waves the priority instead (-1: 1 until the primary segment is done; -2: 2 until then,
-// 1 through the walk, 0 for the fold).
-#ifndef RT_PRIO
-#define RT_PRIO 0
-#endif
+// STATS: the diagnostic build that also tallies the work actually executed (not timed).
+template <int K, bool GPOW, int SMAX, bool STATS>
 __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p) {
-    if constexpr (RT_PRIO < 0) __builtin_amdgcn_s_setprio(-RT_PRIO);
-    constexpr int LDS_LEVELS = StackFor<K, SCRATCH>::lds_levels;  // LdsStack slots, else unused
+    constexpr int LDS_LEVELS = StackFor<K>::lds_levels;  // LdsStack slots, else unused
     __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
     __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * WG_THREADS : 1];
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const TilePixel tpx = tile_pixel(p, blockIdx.x * TILE_W + (wave % WG_WX) * 8 + (lane & 7),
-                                     blockIdx.y * TILE_H + (wave / WG_WX) * 8 + (lane >> 3));
+    const TilePixel tpx = tile_pixel(p, blockIdx.x * TILE_W + (lane & 7), blockIdx.y * TILE_H + (lane >> 3));
     const int x = tpx.x, r = tpx.r, y = tpx.y;
     const bool valid = tpx.valid;
     const unsigned long long pmask = (RT_PRIM_BOX && p.prim_const) ? prim_box_mask(p, x, y) : 0;
 
+    Tally<STATS> tl;
     unsigned cnt = 0;  // packed: reflected segments (bits 0-7) | shadow rays << CNT_SHADOW_SHIFT
     if (valid) {
         const f3 cam = mk(p.cam[0], p.cam[1], p.cam[2]);
@@ -923,13 +656,10 @@ __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p
         f3 d = normalize(sub(vp, cam));
         f3 o = cam;
 
-        typename StackFor<K, SCRATCH>::overflow ovf;
-        typename StackFor<K, SCRATCH>::type stk(&ovf, stk_lv, stk_dv);
+        typename StackFor<K>::type stk(stk_lv, stk_dv);
         stk.origin(d);
         f3 leaf = mk(0.0f, 0.0f, 0.0f);
-        Hit h = nearest_direct<true, SMAX>(p, o, d, pmask);
-        if constexpr (RT_PRIO >= 2 || RT_PRIO == -2) __builtin_amdgcn_s_setprio(1);
-        if constexpr (RT_PRIO == -1) __builtin_amdgcn_s_setprio(0);
+        Hit h = nearest_direct<true, SMAX>(p, o, d, tl, pmask);
         int count = 0;
         for (;;) {
             if (h.prim == HIT_NONE) break;      // nothing hit: plane colour stays Zero
@@ -944,39 +674,31 @@ __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p
             stk.push(make_float4(hp.x, hp.y, hp.z, h.t), make_float4(d.x, d.y, d.z, __int_as_float(h.prim)));
             const int prim = is_sphere ? h.prim : ~h.prim;
             const uint32_t flags = p.mat[is_sphere ? prim : p.S + prim].flags;
-            if (!(flags & MAT_MIRROR) || RT_ABLATE == 3) break;
+            if (!(flags & MAT_MIRROR)) break;
             o = reflect_at(p, o, d, h.t, h.prim);  // :854, CalculateReflectionRay :718-720
             ++count;
             ++cnt;
             // count is the same for every lane still walking: no divergence here
-            h = (RT_TERMINAL && count > p.limit) ? terminal_direct<SMAX>(p, o, d) : nearest_direct<false, SMAX>(p, o, d);
+            h = (RT_TERMINAL && count > p.limit) ? terminal_direct<SMAX>(p, o, d, tl)
+                                                 : nearest_direct<false, SMAX>(p, o, d, tl);
         }
         // backward fold: every recorded hit is shaded in reverse order; a mirror hit
         // consumes the colour of the segment after it (levels 0..limit push at most one
         // record each, so K = limit + 1 records suffice)
         f3 col = leaf;
-        if constexpr (RT_ABLATE == 1) {  // keep the walk alive: fold the records' t into the colour
-            while (stk.n > 0) {
-                float4 ra, rb;
-                stk.pop(p, ra, rb);
-                col.x += ra.w;
-            }
-        }
-        if constexpr (RT_PRIO >= 1) __builtin_amdgcn_s_setprio(RT_PRIO >= 2 ? 2 : 1);
-        if constexpr (RT_PRIO == -2) __builtin_amdgcn_s_setprio(0);
-        while (RT_ABLATE != 1 && stk.n > 0) {
+        while (stk.n > 0) {
             float4 ra, rb;
             stk.pop(p, ra, rb);
             const int code = __float_as_int(rb.w);
             const bool is_s = code >= 0;
-            col = shade_direct<GPOW, SMAX>(p, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z), ra.w, col,
-                              &cnt);
+            col = shade_direct<GPOW, SMAX>(p, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z),
+                                           ra.w, col, &cnt, tl);
         }
         const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
         store_pixel(p, r, y, x, px32);
     }
 
-    add_counters(p, lane, wave, valid ? 1u : 0u, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT);
+    add_counters<STATS>(p, lane, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1032,27 +754,11 @@ __device__ __forceinline__ float wave_max(float v) {
     const unsigned d = (unsigned)__builtin_amdgcn_readlane(__float_as_int(v), 48);
     return __uint_as_float(max(max(a, b), max(c, d)));
 }
-__device__ __forceinline__ float len3(f3 v) { return __builtin_sqrtf(dot(v, v)); }
 // Culling-only arithmetic (never feeds a result): hardware sqrt / rsq (about 1 ulp) instead of
 // the correctly rounded sequences; the cull margins (2^-10 relative on R and delta, 2^-8 on
 // the tests) are orders of magnitude above that error.
-#ifndef RT_FAST_CULL
-#define RT_FAST_CULL 1
-#endif
-__device__ __forceinline__ float clen3(f3 v) {
-#if RT_FAST_CULL
-    return __builtin_amdgcn_sqrtf(dot(v, v));
-#else
-    return len3(v);
-#endif
-}
-__device__ __forceinline__ f3 cnormalize(f3 v) {
-#if RT_FAST_CULL
-    return scale(v, __builtin_amdgcn_rsqf(dot(v, v)));
-#else
-    return normalize(v);
-#endif
-}
+__device__ __forceinline__ float clen3(f3 v) { return __builtin_amdgcn_sqrtf(dot(v, v)); }
+__device__ __forceinline__ f3 cnormalize(f3 v) { return scale(v, __builtin_amdgcn_rsqf(dot(v, v))); }
 __device__ __forceinline__ f3 cross3(f3 l, f3 r) {
     return mk(l.y * r.z - l.z * r.y, l.z * r.x - l.x * r.z, l.x * r.y - l.y * r.x);
 }
@@ -1101,19 +807,11 @@ __device__ __forceinline__ unsigned long long cull_mask(const LaunchParams& p, c
     if (lane < n) {
         cand = true;
         if (B.ok) {
-#if RT_FAST_CULL
             const DevSphereCull s = p.scull[base + lane];
             const f3 w = sub(mk(s.cx, s.cy, s.cz), B.O);
             const float dc = clen3(w) * (1.0f + 0x1p-20f);
             if (s.rr >= 0x1p-50f && dc >= 0x1p-30f && dc < 0x1p40f) {
                 const float rr = s.rr;
-#else
-            const DevSphere s = p.sph[base + lane];
-            const f3 w = sub(mk(s.cx, s.cy, s.cz), B.O);
-            const float dc = len3(w);
-            if (s.r2 >= 0x1p-100f && dc >= 0x1p-30f && dc < 0x1p40f) {
-                const float rr = __builtin_sqrtf(s.r2) * (1.0f + 0x1p-8f);
-#endif
                 const float mgn = 0x1p-8f * (dc + B.R);
                 const float x = clen3(cross3(w, B.A));
                 const bool line = (x - dc * B.delta - B.R) > rr + mgn;
@@ -1132,9 +830,6 @@ __device__ __forceinline__ unsigned long long cull_mask(const LaunchParams& p, c
 // rules (same error analysis and 2^-8 margin as cull_mask, with |u| bounded by the L1 norm
 // of the frame coordinates plus the spreads): line miss if |w_perp| - R_perp > r' + mgn;
 // behind (b >= 0 for every lane) if -w_A - R_neg > mgn, where w = C - O.
-#ifndef RT_SHADOW_CULL
-#define RT_SHADOW_CULL 1
-#endif
 struct ShadowBundle {
     f3 O;
     float Rp, Rneg, Rsum;  // perpendicular spread, backward spread, Rp + Rneg + Rpos
@@ -1200,10 +895,10 @@ __device__ __forceinline__ unsigned long long shadow_cull_mask(const LaunchParam
 // BUNDLE path.  Nearest hit of one segment for every active lane (converged call).  PRIMARY: TracePixel's
 // rule (:977, :987, :993) with the per-frame camera-relative constants; otherwise
 // TraceSecondaryRay's asymmetric rule (:804-806, :819-821, :825).
-
-template <bool PRIMARY>
-__device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d, bool active,
-                                              unsigned long long pmask = 0) {
+// `planes`: the segment's nearest plane hit when the caller already has it (terminal segments).
+template <bool PRIMARY, typename T>
+__device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d, bool active, T& tl,
+                                              unsigned long long pmask = 0, const Hit* planes = nullptr) {
     const unsigned long long am = __builtin_amdgcn_ballot_w64(active);
     if (am == 0) return Hit{0.0f, HIT_NONE};
     // primary segment: the per-frame screen boxes replace the bundle cull
@@ -1229,6 +924,7 @@ __device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d,
         while (m) {
             const int i = base + (int)__builtin_ctzll(m);
             m &= m - 1;
+            tl.sphere(active);
             float t;
             if (PRIMARY && p.prim_const) {
                 // o == camera: oc = cam - c and c = oc.oc - r^2 are per-frame constants (:614-619)
@@ -1255,11 +951,17 @@ __device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d,
     }
     float best_p = __builtin_inff();
     int win_p = -1;
-    for (int i = 0; i < p.P; ++i) {
-        const float t = plane_t(o, d, p.pl[i]);
-        if (t > 0.0f && t < best_p) {
-            best_p = t;
-            win_p = i;
+    if (planes) {
+        best_p = planes->t;
+        win_p = planes->prim;
+    } else {
+        for (int i = 0; i < p.P; ++i) {
+            tl.plane(active);
+            const float t = plane_t(o, d, p.pl[i]);
+            if (t > 0.0f && t < best_p) {
+                best_p = t;
+                win_p = i;
+            }
         }
     }
     if (!active) return Hit{0.0f, HIT_NONE};
@@ -1273,9 +975,9 @@ __device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d,
 // the deeper segment `sec`), then each light in order, then ambient.  Inactive lanes
 // return `sec` unchanged.  Shadow rays (IntersectShadowLight :573-582) of the lanes that
 // need them form one bundle per light (common direction = the light position).
-template <bool GPOW>
+template <bool GPOW, typename T>
 __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool is_sphere, int prim, f3 hp, f3 d, float t,
-                                    f3 sec, unsigned* n_shadow) {
+                                           f3 sec, unsigned* n_shadow, T& tl) {
     // idle lanes (act false) carry a copy of an active lane's record: same branches, result dropped
     const DevMaterial& m = p.mat[is_sphere ? prim : p.S + prim];
     const uint32_t flags = m.flags;
@@ -1317,26 +1019,16 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
             const bool need = diff && shadow_matters(ph, l.intensity, att);
             bool blocked = !need;
             if (__builtin_amdgcn_ballot_w64(need) != 0) {  // some lane's pixel depends on this test
-
-#if RT_SHADOW_CULL
+                tl.shadow(need);
                 const ShadowBundle B = make_shadow_bundle(hp, l, need);
-#else
-                Bundle B = make_bundle(hp, lp, need, true);
-                B.ok = B.ok && l_ok && l.a >= 0x1p-40f && l.a <= 0x1p40f;
-#endif
                 const f3 hs = need ? hp : B.O;  // idle lanes mirror a shading lane (results ignored)
-                if constexpr (RT_CULLSTATS == 2) *n_shadow += (unsigned)((threadIdx.x & 63) == 0) << CNT_SHADOW_SHIFT;
-                for (int base = 0; RT_ABLATE != 2 && base < p.S; base += 64) {
+                for (int base = 0; base < p.S; base += 64) {
                     const int n = min(64, p.S - base);
-#if RT_SHADOW_CULL
                     unsigned long long mk64 = shadow_cull_mask(p, B, l, base, n);
-#else
-                    unsigned long long mk64 = cull_mask(p, B, base, n);
-#endif
                     while (mk64) {
                         const int i = base + (int)__builtin_ctzll(mk64);
                         mk64 &= mk64 - 1;
-                        if constexpr (RT_CULLSTATS == 1) *n_shadow += (unsigned)((threadIdx.x & 63) == 0) << CNT_SHADOW_SHIFT;
+                        tl.sphere(!blocked);
                         blocked = blocked | shadow_blocked(hs, l, l_ok, p.sph[i]);  // no short-circuit branch
                         if (__builtin_amdgcn_ballot_w64(!blocked) == 0) break;
                     }
@@ -1352,7 +1044,7 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
             }
             if (diff) col = add(col, term);
         }
-        if (diff && !RT_CULLSTATS) *n_shadow += (unsigned)p.L << CNT_SHADOW_SHIFT;
+        if (diff) *n_shadow += (unsigned)p.L << CNT_SHADOW_SHIFT;
     }
     col = add(col, mk(m.amb[0], m.amb[1], m.amb[2]));
     return act ? col : sec;
@@ -1360,18 +1052,17 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
 
 // BUNDLE kernel (scenes with >= CULL_MIN_SPHERES spheres): converged control flow so that
 // every segment and every light can form a wave bundle and cull the sphere list.
-template <int K, bool SCRATCH, bool GPOW>
+template <int K, bool GPOW, bool STATS>
 __global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel(LaunchParams p) {
-    constexpr int LDS_LEVELS = StackFor<K, SCRATCH>::lds_levels;  // LdsStack slots, else unused
+    constexpr int LDS_LEVELS = StackFor<K>::lds_levels;  // LdsStack slots, else unused
     __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
     __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * WG_THREADS : 1];
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const TilePixel tpx = tile_pixel(p, blockIdx.x * TILE_W + (wave % WG_WX) * 8 + (lane & 7),
-                                     blockIdx.y * TILE_H + (wave / WG_WX) * 8 + (lane >> 3));
+    const TilePixel tpx = tile_pixel(p, blockIdx.x * TILE_W + (lane & 7), blockIdx.y * TILE_H + (lane >> 3));
     const int x = tpx.x, r = tpx.r, y = tpx.y;
     const bool valid = tpx.valid;
 
+    Tally<STATS> tl;
     unsigned cnt = 0;  // packed: reflected segments (bits 0-7) | shadow rays << CNT_SHADOW_SHIFT
     const f3 cam = mk(p.cam[0], p.cam[1], p.cam[2]);
     // TracePixel primary ray, :963-971 (no half-pixel offset)
@@ -1385,13 +1076,12 @@ __global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel(LaunchParams p
 
     // forward walk: all lanes advance one segment per iteration (converged loop), each
     // shaded hit pushes a record; mirror hits continue with the reflected segment
-    typename StackFor<K, SCRATCH>::overflow ovf;
-    typename StackFor<K, SCRATCH>::type stk(&ovf, stk_lv, stk_dv);
-        stk.origin(d);
+    typename StackFor<K>::type stk(stk_lv, stk_dv);
+    stk.origin(d);
     f3 leaf = mk(0.0f, 0.0f, 0.0f);
     bool active = valid;
     const unsigned long long pmask = (RT_PRIM_BOX && p.prim_const) ? prim_box_mask(p, x, y) : 0;
-    Hit h = nearest_bundle<true>(p, o, d, active, pmask);
+    Hit h = nearest_bundle<true>(p, o, d, active, tl, pmask);
     for (int count = 0;; ++count) {
         if (active) {
             const bool is_sphere = h.prim >= 0;
@@ -1405,7 +1095,7 @@ __global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel(LaunchParams p
                 stk.push(make_float4(hp.x, hp.y, hp.z, h.t), make_float4(d.x, d.y, d.z, __int_as_float(h.prim)));
                 const int prim = is_sphere ? h.prim : ~h.prim;
                 const uint32_t flags = p.mat[is_sphere ? prim : p.S + prim].flags;
-                if (!(flags & MAT_MIRROR) || RT_ABLATE == 3) {
+                if (!(flags & MAT_MIRROR)) {
                     active = false;
                 } else {
                     o = reflect_at(p, o, d, h.t, h.prim);  // :854, CalculateReflectionRay :718-720
@@ -1420,6 +1110,7 @@ __global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel(LaunchParams p
             float best_p = __builtin_inff();
             int win_p = -1;
             for (int i = 0; i < p.P; ++i) {
+                tl.plane(active);
                 const float t = plane_t(o, d, p.pl[i]);
                 if (t > 0.0f && t < best_p) {
                     best_p = t;
@@ -1429,11 +1120,12 @@ __global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel(LaunchParams p
             const bool need = active && win_p >= 0 && best_p - 0.01f > 0.0f;
             h = Hit{0.0f, HIT_NONE};
             if (__builtin_amdgcn_ballot_w64(need) != 0) {
-                const Hit hn = nearest_bundle<false>(p, o, d, need);
+                const Hit pl{best_p, win_p};  // (idle lanes: replaced by a copy of an active lane's ray)
+                const Hit hn = nearest_bundle<false>(p, o, d, need, tl, 0, &pl);
                 if (need) h = hn;
             }
         } else {
-            h = nearest_bundle<false>(p, o, d, active);
+            h = nearest_bundle<false>(p, o, d, active, tl);
         }
     }
 
@@ -1443,14 +1135,6 @@ __global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel(LaunchParams p
     f3 col = leaf;
     const int depth = stk.n;
     int level = (int)wave_max((float)depth);
-    if constexpr (RT_ABLATE == 1) {  // keep the walk alive: fold the records' t into the colour
-        while (stk.n > 0) {
-            float4 ra, rb;
-            stk.pop(p, ra, rb);
-            col.x += ra.w;
-        }
-        level = 0;
-    }
     while (level-- > 0) {
         const bool act = level < depth;  // this lane's top record is at `level`
         float4 ra = make_float4(0.0f, 0.0f, 0.0f, 1.0f), rb = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
@@ -1469,15 +1153,15 @@ __global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel(LaunchParams p
         }
         const int code = __float_as_int(rb.w);
         const bool is_s = code >= 0;
-        col = shade_bundle<GPOW>(p, act, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z), ra.w, col,
-                          &cnt);
+        col = shade_bundle<GPOW>(p, act, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z), ra.w,
+                                 col, &cnt, tl);
     }
     if (valid) {
         const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
         store_pixel(p, r, y, x, px32);
     }
 
-    add_counters(p, lane, wave, valid ? 1u : 0u, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT);
+    add_counters<STATS>(p, lane, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1503,7 +1187,8 @@ __global__ __launch_bounds__(256) void debug_segments_kernel(LaunchParams p, int
                       scale(mk(p.fwd[0], p.fwd[1], p.fwd[2]), 1.0f * p.nearc));
     f3 d = normalize(sub(vp, cam));
     f3 o = cam;
-    Hit h = nearest_direct<true, 0>(p, o, d, p.S >= 64 ? ~0ull : (1ull << p.S) - 1);  // every sphere
+    Tally<false> tl;
+    Hit h = nearest_direct<true, 0>(p, o, d, tl, p.S >= 64 ? ~0ull : (1ull << p.S) - 1);  // every sphere
     for (int level = 0;; ++level) {
         const bool none = h.prim == HIT_NONE;
         append_segment(out, cap, count, o, add(o, scale(d, none ? 100.0f : h.t)), level == 0 ? 0 : 1,
@@ -1537,7 +1222,7 @@ __global__ __launch_bounds__(256) void debug_segments_kernel(LaunchParams p, int
                                     : mk(p.pl[prim].nx, p.pl[prim].ny, p.pl[prim].nz);
         d = sub(d, scale(normal, 2.0f * dot(d, normal)));
         o = hp;
-        h = nearest_direct<false, 0>(p, o, d);
+        h = nearest_direct<false, 0>(p, o, d, tl);
     }
 }
 
@@ -1578,28 +1263,40 @@ __global__ __launch_bounds__(256) void scatter_gathered_kernel(const unsigned ch
     }
 }
 
-#define RT_DEFINE_DISPATCH(FN, NAME, ...)                                                        \
-    template <bool GPOW>                                                                         \
-    static void FN(const LaunchParams& p, dim3 grid, dim3 block, hipStream_t s) {                \
-        const int need = p.limit + 1; /* levels 0..limit can push a record */                    \
-        if (need <= 1)                                                                           \
-            hipLaunchKernelGGL((NAME<1, false, GPOW __VA_ARGS__>), grid, block, 0, s, p);        \
-        else if (need <= 2)                                                                      \
-            hipLaunchKernelGGL((NAME<2, false, GPOW __VA_ARGS__>), grid, block, 0, s, p);        \
-        else if (need <= 4)                                                                      \
-            hipLaunchKernelGGL((NAME<4, false, GPOW __VA_ARGS__>), grid, block, 0, s, p);        \
-        else if (need <= 6)                                                                      \
-            hipLaunchKernelGGL((NAME<6, false, GPOW __VA_ARGS__>), grid, block, 0, s, p);        \
-        else if (need <= 8)                                                                      \
-            hipLaunchKernelGGL((NAME<8, false, GPOW __VA_ARGS__>), grid, block, 0, s, p);        \
-        else                                                                                     \
-            hipLaunchKernelGGL((NAME<64, true, GPOW __VA_ARGS__>), grid, block, 0, s, p);        \
-    }
-RT_DEFINE_DISPATCH(launch_direct_loop, trace_direct_kernel, , 0)
-RT_DEFINE_DISPATCH(launch_bundle, trace_bundle_kernel)
-#undef RT_DEFINE_DISPATCH
+// Instantiation per recursion depth: K = limit + 1 records (levels 0..limit each push at most
+// one), rounded up to the LDS stack sizes; deeper limits use the scratch stack.
+template <template <int> class KERNEL>
+static void launch_by_depth(const LaunchParams& p, dim3 grid, dim3 block, hipStream_t s) {
+    const int need = p.limit + 1;
+    if (need <= 1) hipLaunchKernelGGL(KERNEL<1>::fn, grid, block, 0, s, p);
+    else if (need <= 2) hipLaunchKernelGGL(KERNEL<2>::fn, grid, block, 0, s, p);
+    else if (need <= 4) hipLaunchKernelGGL(KERNEL<4>::fn, grid, block, 0, s, p);
+    else if (need <= 6) hipLaunchKernelGGL(KERNEL<6>::fn, grid, block, 0, s, p);
+    else if (need <= 8) hipLaunchKernelGGL(KERNEL<8>::fn, grid, block, 0, s, p);
+    else hipLaunchKernelGGL(KERNEL<64>::fn, grid, block, 0, s, p);
+}
+template <bool GPOW, bool STATS>
+struct DirectK {
+    template <int K>
+    struct at {
+        static constexpr auto fn = trace_direct_kernel<K, GPOW, 0, STATS>;
+    };
+};
+template <bool GPOW, bool STATS>
+struct BundleK {
+    template <int K>
+    struct at {
+        static constexpr auto fn = trace_bundle_kernel<K, GPOW, STATS>;
+    };
+};
 
-int launch_trace(const LaunchParams& p, bool generic_pow, void* stream) {
+template <bool GPOW, bool STATS>
+static void launch_variant(const LaunchParams& p, bool bundle, dim3 grid, dim3 block, hipStream_t s) {
+    if (bundle) launch_by_depth<BundleK<GPOW, STATS>::template at>(p, grid, block, s);
+    else launch_by_depth<DirectK<GPOW, STATS>::template at>(p, grid, block, s);
+}
+
+int launch_trace(const LaunchParams& p, bool generic_pow, bool stats, void* stream) {
     if (p.local_rows <= 0 || p.W <= 0) return (int)hipSuccess;
     const dim3 grid((unsigned)((p.W + TILE_W - 1) / TILE_W), (unsigned)((p.local_rows + TILE_H - 1) / TILE_H),
                     (unsigned)(p.n_frames > 1 ? p.n_frames : 1));
@@ -1608,12 +1305,12 @@ int launch_trace(const LaunchParams& p, bool generic_pow, void* stream) {
     // bundle culling pays for its per-wave bounds only with enough spheres (A/B: +15 % at
     // 8 spheres, 3x faster at 64)
     const bool bundle = p.S >= CULL_MIN_SPHERES;
-    if (generic_pow) {
-        if (bundle) launch_bundle<true>(p, grid, block, s);
-        else launch_direct_loop<true>(p, grid, block, s);
+    if (stats) {
+        if (generic_pow) launch_variant<true, true>(p, bundle, grid, block, s);
+        else launch_variant<false, true>(p, bundle, grid, block, s);
     } else {
-        if (bundle) launch_bundle<false>(p, grid, block, s);
-        else launch_direct_loop<false>(p, grid, block, s);
+        if (generic_pow) launch_variant<true, false>(p, bundle, grid, block, s);
+        else launch_variant<false, false>(p, bundle, grid, block, s);
     }
     return (int)hipGetLastError();
 }

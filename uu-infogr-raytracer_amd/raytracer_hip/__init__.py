@@ -76,10 +76,12 @@ class Surface:
 class Context:
     """Thin owner of an rt_ctx*."""
 
-    def __init__(self, n_gpus: int = 1):
+    def __init__(self, n_gpus: int = 1, flags: int = 0):
+        """flags: abi.RT_CREATE_RCCL_GATHER routes rt_render through the multi-GPU band +
+        RCCL-gather path even on one device (rt_create_ex)."""
         self.lib = load_library()
         self.ptr = C.c_void_p()
-        check(self.lib, self.lib.rt_create(int(n_gpus), C.byref(self.ptr)))
+        check(self.lib, self.lib.rt_create_ex(int(n_gpus), int(flags), C.byref(self.ptr)))
         self.n_gpus = n_gpus
         self.scene = None
 
@@ -221,6 +223,12 @@ class Context:
 
     def reset_stats(self):
         self._check(self.lib.rt_reset_stats(self.ptr))
+
+    def count_work(self, width: int, height: int) -> dict:
+        """Nominal and executed work of one frame of the current camera (rt_count_work)."""
+        w = abi.rt_work()
+        self._check(self.lib.rt_count_work(self.ptr, width, height, C.byref(w)))
+        return w.as_dict()
 
     def set_timing(self, every: int):
         """Time every `every`-th launch/copy/gather with HIP events (0 = none; default 64)."""

@@ -14,7 +14,8 @@ PKG_ROOT = os.path.dirname(_HERE)
 # RAYTRACER_HIP_LIB selects another build of the library (A/B variants under lib/ab/)
 LIB_PATH = os.environ.get("RAYTRACER_HIP_LIB") or os.path.join(PKG_ROOT, "lib", "libraytracer_hip.so")
 
-RT_ABI_VERSION = 4  # include/raytracer_hip.h
+RT_ABI_VERSION = 5  # include/raytracer_hip.h
+RT_CREATE_RCCL_GATHER = 1
 RT_BANDS_INT32, RT_BANDS_RGB24, RT_BANDS_FRAME = 0, 1, 2
 RT_OK = 0
 RT_ERR_INVALID_ARG = -1
@@ -81,6 +82,17 @@ class rt_stats(C.Structure):
         return {name: getattr(self, name) for name, _ in self._fields_}
 
 
+class rt_work(C.Structure):
+    _fields_ = [
+        ("primary_rays", C.c_uint64), ("reflect_rays", C.c_uint64), ("shadow_rays", C.c_uint64),
+        ("sphere_tests", C.c_uint64), ("plane_tests", C.c_uint64), ("shadow_rays_run", C.c_uint64),
+        ("sphere_tests_run", C.c_uint64), ("plane_tests_run", C.c_uint64),
+    ]
+
+    def as_dict(self):
+        return {name: getattr(self, name) for name, _ in self._fields_}
+
+
 class rt_wire_layout(C.Structure):
     _fields_ = [
         ("fixed_bytes", C.c_uint64), ("max_bytes", C.c_uint64), ("tiles_x", C.c_int32), ("tiles_y", C.c_int32),
@@ -94,6 +106,7 @@ EXPORTS = [
     ("rt_device_count", C.c_int, [C.POINTER(C.c_int)]),
     ("rt_last_error", C.c_char_p, [C.c_void_p]),
     ("rt_create", C.c_int, [C.c_int, C.POINTER(C.c_void_p)]),
+    ("rt_create_ex", C.c_int, [C.c_int, C.c_int, C.POINTER(C.c_void_p)]),
     ("rt_destroy", None, [C.c_void_p]),
     ("rt_set_scene", C.c_int, [C.c_void_p, C.POINTER(rt_sphere), C.c_int, C.POINTER(rt_plane), C.c_int,
                                C.POINTER(rt_light), C.c_int, rt_vec3, C.c_int]),
@@ -128,6 +141,7 @@ EXPORTS = [
     ("rt_set_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_get_stats", C.c_int, [C.c_void_p, C.POINTER(rt_stats)]),
     ("rt_reset_stats", C.c_int, [C.c_void_p]),
+    ("rt_count_work", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(rt_work)]),
 ]
 
 _lib = None
