@@ -244,6 +244,7 @@ def measure_single(ctx, sc, args, torch, abi, steps, warmup):
     while (time.perf_counter() - t_w) * 1e3 < args.min_warmup_ms:  # clock ramp (untimed)
         per_frame = (time.perf_counter() - t_w) / max(1, done)
         n = max(1, min(16 * fpl, int((args.min_warmup_ms / 1e3 - (time.perf_counter() - t_w)) / per_frame) + 1))
+        n = -(-n // cap) * cap  # whole launches of `cap` frames: every warm-up launch has the timed shape
         issue(n)
         done += n
         torch.cuda.synchronize()

@@ -394,6 +394,32 @@ __device__ __forceinline__ void for_spheres(int S, F&& f) {
     }
 }
 
+// The sphere table of the direct path's wave-uniform loops (sphere records for secondary and
+// shadow rays, camera-relative constants of the primary segment).  SMAX = 0: read from memory in
+// every iteration (scalar loads); SMAX > 0 (scenes with S <= SMAX, loops unrolled): loaded once
+// per wave into SGPRs -- no scalar-load round trip inside the loops.  Entries i >= S are never
+// used (uniform `i < S` guards); reading them stays inside the scene allocation (256-byte
+// aligned sections) and the kernarg's MAX_PRIM_CONST entries.
+template <int SMAX, bool REG = (SMAX > 0)>
+struct SphereTab {
+    const DevSphere* g;
+    const PrimConst* gp;
+    __device__ __forceinline__ explicit SphereTab(const LaunchParams& p) : g(p.sph), gp(p.pc) {}
+    __device__ __forceinline__ DevSphere s(int i) const { return g[i]; }
+    __device__ __forceinline__ PrimConst pc(int i) const { return gp[i]; }
+};
+template <int SMAX>
+struct SphereTab<SMAX, true> {
+    DevSphere r[SMAX];
+    const PrimConst* gp;
+    __device__ __forceinline__ explicit SphereTab(const LaunchParams& p) : gp(p.pc) {
+#pragma unroll
+        for (int i = 0; i < SMAX; ++i) r[i] = p.sph[i];
+    }
+    __device__ __forceinline__ DevSphere s(int i) const { return r[i]; }
+    __device__ __forceinline__ PrimConst pc(int i) const { return gp[i]; }
+};
+
 // Result of a nearest-hit search.
 struct Hit {
     float t;
@@ -422,8 +448,8 @@ __device__ __forceinline__ bool shadow_matters(f3 ph, float intensity, float att
 }
 
 template <bool GPOW, int SMAX, typename T>
-__device__ __forceinline__ f3 shade_direct(const LaunchParams& p, bool is_sphere, int prim, f3 hp, f3 d, float t, f3 sec,
-                                           unsigned* n_shadow, T& tl) {
+__device__ __forceinline__ f3 shade_direct(const LaunchParams& p, const SphereTab<SMAX>& tab, bool is_sphere, int prim,
+                                           f3 hp, f3 d, float t, f3 sec, unsigned* n_shadow, T& tl) {
     const DevMaterial& m = p.mat[is_sphere ? prim : p.S + prim];
     const uint32_t flags = m.flags;
     f3 normal;
@@ -466,7 +492,7 @@ __device__ __forceinline__ f3 shade_direct(const LaunchParams& p, bool is_sphere
                     for_spheres<SMAX>(p.S, [&](int i) {
                         if (!blocked) {
                             tl.sphere(true);
-                            blocked = shadow_blocked(hp, l, l_ok, p.sph[i]);
+                            blocked = shadow_blocked(hp, l, l_ok, tab.s(i));
                         }
                     });
                 } else {
@@ -535,7 +561,8 @@ __device__ __forceinline__ TilePixel tile_pixel(const LaunchParams& p, int x, in
 }
 
 template <bool PRIMARY, int SMAX, typename T>
-__device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d, T& tl, unsigned long long pmask = 0) {
+__device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, const SphereTab<SMAX>& tab, f3 o, f3 d, T& tl,
+                                              unsigned long long pmask = 0) {
     const float a = dot(d, d);
     const float a2 = 2.0f * a, a4 = 4.0f * a;
     const bool a2_ok = a2 > 0.0f && a2 < __builtin_inff();
@@ -545,7 +572,7 @@ __device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d,
         // o == camera: oc = cam - c and c = oc.oc - r^2 are the same per frame (:614-619)
         auto test = [&](int i) {
             tl.sphere(true);
-            const PrimConst pc = p.pc[i];
+            const PrimConst pc = tab.pc(i);
             const float b = 2.0f * dot(mk(pc.ocx, pc.ocy, pc.ocz), d);
             const float disc = b * b - a4 * pc.c;
             const float t = a2_ok ? root_t1(b, disc, a2) : root_full(b, disc, a2);
@@ -554,8 +581,12 @@ __device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d,
                 win_s = i;
             }
         };
-        if constexpr (RT_PRIM_BOX) {
+        if constexpr (RT_PRIM_BOX && SMAX > 0) {
             // only the wave's candidate spheres, in ascending order (non-candidates give t <= 0)
+#pragma unroll
+            for (int i = 0; i < SMAX; ++i)
+                if ((pmask >> i) & 1ull) test(i);
+        } else if constexpr (RT_PRIM_BOX) {
             for (unsigned long long m = pmask; m; m &= m - 1) test((int)__builtin_ctzll(m));
         } else {
             for_spheres<SMAX>(p.S, test);
@@ -563,7 +594,7 @@ __device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d,
     } else {
         for_spheres<SMAX>(p.S, [&](int i) {
             tl.sphere(true);
-            const float t = sphere_t(o, d, a2, a4, a2_ok, p.sph[i]);
+            const float t = sphere_t(o, d, a2, a4, a2_ok, tab.s(i));
             if (PRIMARY) {
                 if (t > 0.0f && best_s > t) {
                     best_s = t;
@@ -603,7 +634,7 @@ __device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d,
 #define RT_TERMINAL 1
 #endif
 template <int SMAX, typename T>
-__device__ __forceinline__ Hit terminal_direct(const LaunchParams& p, f3 o, f3 d, T& tl) {
+__device__ __forceinline__ Hit terminal_direct(const LaunchParams& p, const SphereTab<SMAX>& tab, f3 o, f3 d, T& tl) {
     float best_p = __builtin_inff();
     int win_p = -1;
     for (int i = 0; i < p.P; ++i) {
@@ -621,7 +652,7 @@ __device__ __forceinline__ Hit terminal_direct(const LaunchParams& p, f3 o, f3 d
     float best_s = __builtin_inff();
     for_spheres<SMAX>(p.S, [&](int i) {
         tl.sphere(true);
-        const float t = sphere_t(o, d, a2, a4, a2_ok, p.sph[i]);
+        const float t = sphere_t(o, d, a2, a4, a2_ok, tab.s(i));
         const float tm = t - 0.01f;
         if (tm > 0.0f && tm < best_s) best_s = t;
     });
@@ -643,6 +674,7 @@ __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p
     const unsigned long long pmask = (RT_PRIM_BOX && p.prim_const) ? prim_box_mask(p, x, y) : 0;
 
     Tally<STATS> tl;
+    const SphereTab<SMAX> tab(p);
     unsigned cnt = 0;  // packed: reflected segments (bits 0-7) | shadow rays << CNT_SHADOW_SHIFT
     if (valid) {
         const f3 cam = mk(p.cam[0], p.cam[1], p.cam[2]);
@@ -659,7 +691,7 @@ __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p
         typename StackFor<K>::type stk(stk_lv, stk_dv);
         stk.origin(d);
         f3 leaf = mk(0.0f, 0.0f, 0.0f);
-        Hit h = nearest_direct<true, SMAX>(p, o, d, tl, pmask);
+        Hit h = nearest_direct<true, SMAX>(p, tab, o, d, tl, pmask);
         int count = 0;
         for (;;) {
             if (h.prim == HIT_NONE) break;      // nothing hit: plane colour stays Zero
@@ -679,8 +711,8 @@ __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p
             ++count;
             ++cnt;
             // count is the same for every lane still walking: no divergence here
-            h = (RT_TERMINAL && count > p.limit) ? terminal_direct<SMAX>(p, o, d, tl)
-                                                 : nearest_direct<false, SMAX>(p, o, d, tl);
+            h = (RT_TERMINAL && count > p.limit) ? terminal_direct<SMAX>(p, tab, o, d, tl)
+                                                 : nearest_direct<false, SMAX>(p, tab, o, d, tl);
         }
         // backward fold: every recorded hit is shaded in reverse order; a mirror hit
         // consumes the colour of the segment after it (levels 0..limit push at most one
@@ -691,8 +723,8 @@ __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p
             stk.pop(p, ra, rb);
             const int code = __float_as_int(rb.w);
             const bool is_s = code >= 0;
-            col = shade_direct<GPOW, SMAX>(p, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z),
-                                           ra.w, col, &cnt, tl);
+            col = shade_direct<GPOW, SMAX>(p, tab, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z),
+                                           mk(rb.x, rb.y, rb.z), ra.w, col, &cnt, tl);
         }
         const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
         store_pixel(p, r, y, x, px32);
@@ -1188,7 +1220,8 @@ __global__ __launch_bounds__(256) void debug_segments_kernel(LaunchParams p, int
     f3 d = normalize(sub(vp, cam));
     f3 o = cam;
     Tally<false> tl;
-    Hit h = nearest_direct<true, 0>(p, o, d, tl, p.S >= 64 ? ~0ull : (1ull << p.S) - 1);  // every sphere
+    const SphereTab<0> tab(p);
+    Hit h = nearest_direct<true, 0>(p, tab, o, d, tl, p.S >= 64 ? ~0ull : (1ull << p.S) - 1);  // every sphere
     for (int level = 0;; ++level) {
         const bool none = h.prim == HIT_NONE;
         append_segment(out, cap, count, o, add(o, scale(d, none ? 100.0f : h.t)), level == 0 ? 0 : 1,
@@ -1222,7 +1255,7 @@ __global__ __launch_bounds__(256) void debug_segments_kernel(LaunchParams p, int
                                     : mk(p.pl[prim].nx, p.pl[prim].ny, p.pl[prim].nz);
         d = sub(d, scale(normal, 2.0f * dot(d, normal)));
         o = hp;
-        h = nearest_direct<false, 0>(p, o, d, tl);
+        h = nearest_direct<false, 0>(p, tab, o, d, tl);
     }
 }
 
@@ -1275,13 +1308,18 @@ static void launch_by_depth(const LaunchParams& p, dim3 grid, dim3 block, hipStr
     else if (need <= 8) hipLaunchKernelGGL(KERNEL<8>::fn, grid, block, 0, s, p);
     else hipLaunchKernelGGL(KERNEL<64>::fn, grid, block, 0, s, p);
 }
-template <bool GPOW, bool STATS>
+template <bool GPOW, bool STATS, int SMAX>
 struct DirectK {
     template <int K>
     struct at {
-        static constexpr auto fn = trace_direct_kernel<K, GPOW, 0, STATS>;
+        static constexpr auto fn = trace_direct_kernel<K, GPOW, SMAX, STATS>;
     };
 };
+// RT_SREG: scenes with S <= SREG_MAX spheres run the direct kernel with the sphere table in SGPRs
+#ifndef RT_SREG
+#define RT_SREG 0
+#endif
+constexpr int SREG_MAX = 8;
 template <bool GPOW, bool STATS>
 struct BundleK {
     template <int K>
@@ -1293,7 +1331,8 @@ struct BundleK {
 template <bool GPOW, bool STATS>
 static void launch_variant(const LaunchParams& p, bool bundle, dim3 grid, dim3 block, hipStream_t s) {
     if (bundle) launch_by_depth<BundleK<GPOW, STATS>::template at>(p, grid, block, s);
-    else launch_by_depth<DirectK<GPOW, STATS>::template at>(p, grid, block, s);
+    else if (RT_SREG && p.S <= SREG_MAX) launch_by_depth<DirectK<GPOW, STATS, SREG_MAX>::template at>(p, grid, block, s);
+    else launch_by_depth<DirectK<GPOW, STATS, 0>::template at>(p, grid, block, s);
 }
 
 int launch_trace(const LaunchParams& p, bool generic_pow, bool stats, void* stream) {
