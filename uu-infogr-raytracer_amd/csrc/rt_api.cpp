@@ -527,8 +527,12 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
     SceneLayout L;
     L.S = n_spheres, L.P = n_planes, L.L = n_lights, L.limit = recursion_limit;
     auto al = [](size_t v) { return (v + 255) & ~(size_t)255; };
+    // the sphere table is padded to an even count (the direct kernel's loops take spheres in
+    // pairs) with a sphere that never hits: NaN centre and radius^2 make every comparison of
+    // IntersectsSphere false (no candidate, t = 0, no shadow)
+    const int s_pad = n_spheres + (n_spheres & 1);
     L.off_sph = 0;
-    L.off_mat = al(L.off_sph + sizeof(DevSphere) * (size_t)n_spheres);
+    L.off_mat = al(L.off_sph + sizeof(DevSphere) * (size_t)s_pad);
     L.off_pl = al(L.off_mat + sizeof(DevMaterial) * (size_t)(n_spheres + n_planes));
     L.off_li = al(L.off_pl + sizeof(DevPlane) * (size_t)n_planes);
     L.off_cull = al(L.off_li + sizeof(DevLight) * (size_t)n_lights);
@@ -548,6 +552,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
         const double rr = std::sqrt((double)sph[i].r2) * (1.0 + 0x1p-8);
         cull[i] = DevSphereCull{sph[i].cx, sph[i].cy, sph[i].cz, std::nextafter((float)rr, INFINITY)};
     }
+    for (int i = n_spheres; i < s_pad; ++i) sph[i] = DevSphere{NAN, NAN, NAN, NAN};
     L.host_sph.assign(sph, sph + n_spheres);
     for (int i = 0; i < n_planes; ++i) {
         const rt_plane& p = planes[i];

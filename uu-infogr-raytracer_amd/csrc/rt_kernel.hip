@@ -120,18 +120,26 @@ __device__ __forceinline__ float spec_pow(float x, const DevMaterial& m) {
 // exactly-rounded results satisfy t2 >= t1 (numerators ordered, rounding and division by
 // a positive number monotonic), so a selectable distance exists iff t1 > 0, and then it is
 // t1 itself.  t1 > 0 iff fl(-b - sq) > 0 iff -b > sq (gradual underflow), which needs
-// -b > 0 first.  So: no sqrt when b >= 0, no division unless -b > sq, never the t2
-// division.  Returns the reference's distance or 0 (non-selectable) -- identical
-// selections and identical winning distances.
+// -b > 0 first.  So: no sqrt when b >= 0, never the t2 division.  Returns the reference's
+// distance when it is selectable and otherwise a value <= 0 or NaN, which every caller's
+// selection test (t > 0, t - 0.01 > 0) rejects exactly as it rejects the reference's 0:
+// fl(-b - sq) <= 0 whenever -b <= sq (and NaN when disc < 0), and dividing by the positive
+// 2a keeps the sign -- identical selections and identical winning distances.
+//
+// Scalar-issue economy (MI355X: one scalar unit per CU serves its 4 SIMDs, ~1 SALU
+// instruction per CU-cycle against ~1.8 VALU, profiles/r02_issue_probe.txt): the sqrt and the
+// division run under a wave-uniform branch on the ballot of the candidate lanes instead of an
+// exec-mask if/else, and the result needs no select.
 // ---------------------------------------------------------------------------------
+__device__ __forceinline__ bool sphere_candidate(float b, float disc) {
+    // disc >= 0 && b <= 0 (b = +-0 cannot select: -b > sq fails); NaN -> false
+    return __builtin_elementwise_minimum(disc, -b) >= 0.0f;
+}
 __device__ __forceinline__ float root_t1(float b, float disc, float a2) {
     float t = 0.0f;
-    if (disc >= 0.0f && b < 0.0f) {
-        const float sq = cr_sqrt(disc);  // == (float)Math.Sqrt((double)disc)
-        const float nb = -b;
-        const bool sel = nb > sq;
-        const float q = cr_div_if(sel, nb - sq, a2);  // predicated, not branched
-        t = sel ? q : 0.0f;
+    if (__builtin_amdgcn_ballot_w64(sphere_candidate(b, disc)) != 0) {  // wave-uniform
+        const float sq = cr_sqrt(disc);  // == (float)Math.Sqrt((double)disc); NaN off-candidate
+        t = (-b - sq) / a2;              // t1 = (-b - sqrt) / 2a, :630
     }
     return t;
 }
@@ -148,30 +156,33 @@ __device__ __forceinline__ float root_full(float b, float disc, float a2) {
     return t;
 }
 
+// A2OK: 2a is finite and > 0 for every active lane (checked once per segment with a ballot,
+// so the sphere loops carry no per-lane two-way split).
+template <bool A2OK>
 __device__ __forceinline__ float sphere_t(f3 o, f3 d, float a2, float a4, bool a2_ok, const DevSphere& s) {
     const f3 oc = sub(o, mk(s.cx, s.cy, s.cz));
     const float b = 2.0f * dot(oc, d);
     const float c = dot(oc, oc) - s.r2;
     const float disc = b * b - a4 * c;
-    return a2_ok ? root_t1(b, disc, a2) : root_full(b, disc, a2);
+    if constexpr (A2OK) return root_t1(b, disc, a2);
+    else return a2_ok ? root_t1(b, disc, a2) : root_full(b, disc, a2);
 }
 
 // Shadow ray of IntersectShadowLight (origin = hit point, direction = light POSITION,
 // epsilon 0.001, RayTracer.cs:574-578): collision iff min(max(t1-e,0), max(t2-e,0)) > 0.
 // With 2a finite-positive (uniform per light) and t2 >= t1 that is t1 - e > 0 (and then
-// t2 - e > 0 too), which again needs -b > sq.
+// t2 - e > 0 too); fl(-b - sq) / 2a - e > 0 already implies -b > sq (see root_t1).
+template <bool A2OK>
 __device__ __forceinline__ bool shadow_blocked(f3 hp, const DevLight& l, bool a2_ok, const DevSphere& s) {
     const f3 oc = sub(hp, mk(s.cx, s.cy, s.cz));
     const float b = 2.0f * dot(oc, mk(l.px, l.py, l.pz));
     const float c = dot(oc, oc) - s.r2;
     const float disc = b * b - l.a4 * c;
-    if (a2_ok) {
+    if (A2OK || a2_ok) {
         bool hit = false;
-        if (disc >= 0.0f && b < 0.0f) {
+        if (__builtin_amdgcn_ballot_w64(sphere_candidate(b, disc)) != 0) {  // wave-uniform
             const float sq = cr_sqrt(disc);
-            const float nb = -b;
-            const bool sel = nb > sq;
-            hit = sel & (cr_div_if(sel, nb - sq, l.a2) - 0.001f > 0.0f);
+            hit = (-b - sq) / l.a2 - 0.001f > 0.0f;
         }
         return hit;
     }
@@ -185,14 +196,12 @@ __device__ __forceinline__ bool shadow_blocked(f3 hp, const DevLight& l, bool a2
 }
 
 // IntersectPlane, RayTracer.cs:590-604: t = (((-o.x*n.x) - o.y*n.y) - o.z*n.z + c.n) / d.n,
-// hit iff t > 0.  The quotient can only be > 0 when numerator and denominator are nonzero
-// with equal signs; otherwise it is <= 0 or NaN (a miss) and the division is skipped.
+// hit iff t > 0 -- the quotient itself.  (+inf, from a zero denominator, is a "hit" that no
+// nearest-plane search can select: the best distance starts at +inf and the test is strict.)
 __device__ __forceinline__ float plane_t(f3 o, f3 d, const DevPlane& p) {
     const float num = ((-o.x * p.nx - o.y * p.ny) - o.z * p.nz) + p.cn;
     const float den = dot(d, mk(p.nx, p.ny, p.nz));
-    const bool sel = (num > 0.0f && den > 0.0f) || (num < 0.0f && den < 0.0f);
-    const float q = cr_div_if(sel, num, den);
-    return sel ? q : 0.0f;
+    return num / den;
 }
 
 // ShiftColor, :1046-1052: Math.Clamp (NaN passes), * 255f, Math.Floor, (int), (byte).
@@ -380,46 +389,6 @@ __device__ __forceinline__ void add_counters(const LaunchParams& p, int lane, un
     }
 }
 
-// Sphere loop of the direct path: a runtime loop (SMAX = 0, shipped) or fully unrolled over
-// SMAX with uniform `i < S` guards.
-template <int SMAX, typename F>
-__device__ __forceinline__ void for_spheres(int S, F&& f) {
-    if constexpr (SMAX > 0) {
-#pragma unroll
-        for (int i = 0; i < SMAX; ++i)
-            if (i < S) f(i);
-    } else {
-#pragma unroll 2
-        for (int i = 0; i < S; ++i) f(i);
-    }
-}
-
-// The sphere table of the direct path's wave-uniform loops (sphere records for secondary and
-// shadow rays, camera-relative constants of the primary segment).  SMAX = 0: read from memory in
-// every iteration (scalar loads); SMAX > 0 (scenes with S <= SMAX, loops unrolled): loaded once
-// per wave into SGPRs -- no scalar-load round trip inside the loops.  Entries i >= S are never
-// used (uniform `i < S` guards); reading them stays inside the scene allocation (256-byte
-// aligned sections) and the kernarg's MAX_PRIM_CONST entries.
-template <int SMAX, bool REG = (SMAX > 0)>
-struct SphereTab {
-    const DevSphere* g;
-    const PrimConst* gp;
-    __device__ __forceinline__ explicit SphereTab(const LaunchParams& p) : g(p.sph), gp(p.pc) {}
-    __device__ __forceinline__ DevSphere s(int i) const { return g[i]; }
-    __device__ __forceinline__ PrimConst pc(int i) const { return gp[i]; }
-};
-template <int SMAX>
-struct SphereTab<SMAX, true> {
-    DevSphere r[SMAX];
-    const PrimConst* gp;
-    __device__ __forceinline__ explicit SphereTab(const LaunchParams& p) : gp(p.pc) {
-#pragma unroll
-        for (int i = 0; i < SMAX; ++i) r[i] = p.sph[i];
-    }
-    __device__ __forceinline__ DevSphere s(int i) const { return r[i]; }
-    __device__ __forceinline__ PrimConst pc(int i) const { return gp[i]; }
-};
-
 // Result of a nearest-hit search.
 struct Hit {
     float t;
@@ -427,9 +396,27 @@ struct Hit {
 };
 constexpr int HIT_NONE = 0x7fffffff;
 
-// DIRECT path (scenes with < CULL_MIN_SPHERES spheres): per-lane divergent loops.
-// Shading of one shaded hit (TraceSphere :847-873 / TracePlane :736-778): the colour is
-// accumulated in the reference's order -- mirror term (from the deeper segment `sec`),
+// Nearest-hit selection rules as selects (VALU compares and cndmasks, no scalar mask logic):
+// TracePixel (:977, :987): t is taken iff t > 0 && best > t.
+__device__ __forceinline__ void take_primary(float t, int i, float& best, int& win) {
+    const float tt = t > 0.0f ? t : __builtin_inff();
+    const bool b = tt < best;
+    best = b ? tt : best;
+    win = b ? i : win;
+}
+// TraceSecondaryRay (:804-806): t is taken iff t - 0.01 > 0 && t - 0.01 < best, and then
+// best = t (the asymmetric rule, Q5/Q6).
+__device__ __forceinline__ void take_secondary(float t, int i, float& best, int& win) {
+    const float tm = t - 0.01f;
+    const float tt = tm > 0.0f ? tm : __builtin_inff();
+    const bool b = tt < best;
+    best = b ? t : best;
+    win = b ? i : win;
+}
+
+// DIRECT path (scenes with < CULL_MIN_SPHERES spheres): per-lane divergent walks, wave-uniform
+// primitive loops.  Shading of one shaded hit (TraceSphere :847-873 / TracePlane :736-778): the
+// colour is accumulated in the reference's order -- mirror term (from the deeper segment `sec`),
 // then each light, then ambient.  Returns the colour; adds shadow rays to *n_shadow.
 // A light's shadow test can change the pixel only through I * att * phong vs 0 * phong.  When
 // every phong component is +-0 or NaN and I * att is finite, both give +-0 / NaN per
@@ -447,9 +434,31 @@ __device__ __forceinline__ bool shadow_matters(f3 ph, float intensity, float att
     return !(finite && zero_or_nan(ph.x) && zero_or_nan(ph.y) && zero_or_nan(ph.z));
 }
 
-template <bool GPOW, int SMAX, typename T>
-__device__ __forceinline__ f3 shade_direct(const LaunchParams& p, const SphereTab<SMAX>& tab, bool is_sphere, int prim,
-                                           f3 hp, f3 d, float t, f3 sec, unsigned* n_shadow, T& tl) {
+// IntersectShadowLight's sphere loop (:577-579) for the active lanes: a wave-uniform loop over
+// pairs of spheres that ends when every active lane is blocked (the reference's loop has no
+// early exit, but a blocked ray stays blocked).  A lane's result is the OR of its tests, as in
+// the reference.  The scalar unit bounds these kernels (one per CU for 4 SIMDs,
+// profiles/r02_issue_probe.txt), so the loop is shaped for scalar economy: the blocked state is
+// a VGPR value (no lane-mask phi), one 32-byte scalar load and one exit ballot per pair (the
+// device table is padded to an even count with a sphere that never hits, rt_set_scene), no
+// per-lane loop exits (their mask bookkeeping cost ~28 scalar instructions per sphere).
+template <bool A2OK, typename T>
+__device__ __forceinline__ bool shadow_scan(const LaunchParams& p, f3 hp, const DevLight& l, T& tl) {
+    int blk = 0;
+    for (int i = 0; i < p.S; i += 2) {
+        const DevSphere s0 = p.sph[i], s1 = p.sph[i + 1];
+        tl.sphere(blk == 0);
+        blk = shadow_blocked<A2OK>(hp, l, false, s0) ? 1 : blk;
+        tl.sphere((blk == 0) & (i + 1 < p.S));
+        blk = shadow_blocked<A2OK>(hp, l, false, s1) ? 1 : blk;
+        if (__builtin_amdgcn_ballot_w64(blk == 0) == 0) break;
+    }
+    return blk != 0;
+}
+
+template <bool GPOW, typename T>
+__device__ __forceinline__ f3 shade_direct(const LaunchParams& p, bool is_sphere, int prim, f3 hp, f3 d, float t, f3 sec,
+                                           unsigned* n_shadow, T& tl) {
     const DevMaterial& m = p.mat[is_sphere ? prim : p.S + prim];
     const uint32_t flags = m.flags;
     f3 normal;
@@ -488,19 +497,7 @@ __device__ __forceinline__ f3 shade_direct(const LaunchParams& p, const SphereTa
             bool blocked = false;
             if (shadow_matters(ph, l.intensity, att)) {
                 tl.shadow(true);
-                if constexpr (SMAX > 0) {
-                    for_spheres<SMAX>(p.S, [&](int i) {
-                        if (!blocked) {
-                            tl.sphere(true);
-                            blocked = shadow_blocked(hp, l, l_ok, tab.s(i));
-                        }
-                    });
-                } else {
-                    for (int i = 0; i < p.S && !blocked; ++i) {
-                        tl.sphere(true);
-                        blocked = shadow_blocked(hp, l, l_ok, p.sph[i]);
-                    }
-                }
+                blocked = l_ok ? shadow_scan<true>(p, hp, l, tl) : shadow_scan<false>(p, hp, l, tl);
             }
             const float inten = blocked ? 0.0f : l.intensity;
             const float ia = inten * att;
@@ -560,64 +557,60 @@ __device__ __forceinline__ TilePixel tile_pixel(const LaunchParams& p, int x, in
     return t;
 }
 
-template <bool PRIMARY, int SMAX, typename T>
-__device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, const SphereTab<SMAX>& tab, f3 o, f3 d, T& tl,
-                                              unsigned long long pmask = 0) {
+// Sphere part of a nearest-hit search for the active lanes.  PRIMARY with p.prim_const: the
+// per-frame camera-relative constants and the wave's screen-box candidates (pmask); otherwise
+// every sphere (IntersectsSphere, :613-642).  A2OK: 2a finite-positive on every active lane.
+template <bool PRIMARY, bool A2OK, typename T>
+__device__ __forceinline__ void nearest_spheres(const LaunchParams& p, f3 o, f3 d, float a2, float a4, bool a2_ok,
+                                                unsigned long long pmask, float& best_s, int& win_s, T& tl) {
+    if (PRIMARY && p.prim_const) {
+        // o == camera: oc = cam - c and c = oc.oc - r^2 are the same per frame (:614-619);
+        // only the wave's candidate spheres, in ascending order (non-candidates give t <= 0)
+        for (unsigned long long m = RT_PRIM_BOX ? pmask : (p.S >= 64 ? ~0ull : (1ull << p.S) - 1); m;) {
+            const int i = (int)__builtin_ctzll(m);
+            m &= ~(1ull << i);
+            tl.sphere(true);
+            const PrimConst pc = p.pc[i];
+            const float b = 2.0f * dot(mk(pc.ocx, pc.ocy, pc.ocz), d);
+            const float disc = b * b - a4 * pc.c;
+            const float t = A2OK ? root_t1(b, disc, a2) : (a2_ok ? root_t1(b, disc, a2) : root_full(b, disc, a2));
+            take_primary(t, i, best_s, win_s);
+        }
+    } else {
+        // pairs (the device table is padded to an even count with a sphere that never hits)
+        for (int i = 0; i < p.S; i += 2) {
+            const DevSphere s0 = p.sph[i], s1 = p.sph[i + 1];
+            tl.sphere(true);
+            tl.sphere(i + 1 < p.S);
+            const float t0 = sphere_t<A2OK>(o, d, a2, a4, a2_ok, s0);
+            const float t1 = sphere_t<A2OK>(o, d, a2, a4, a2_ok, s1);
+            if (PRIMARY) {
+                take_primary(t0, i, best_s, win_s);
+                take_primary(t1, i + 1, best_s, win_s);
+            } else {
+                take_secondary(t0, i, best_s, win_s);
+                take_secondary(t1, i + 1, best_s, win_s);
+            }
+        }
+    }
+}
+
+template <bool PRIMARY, typename T>
+__device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d, T& tl, unsigned long long pmask = 0) {
     const float a = dot(d, d);
     const float a2 = 2.0f * a, a4 = 4.0f * a;
     const bool a2_ok = a2 > 0.0f && a2 < __builtin_inff();
     float best_s = __builtin_inff();
     int win_s = -1;
-    if (PRIMARY && p.prim_const) {
-        // o == camera: oc = cam - c and c = oc.oc - r^2 are the same per frame (:614-619)
-        auto test = [&](int i) {
-            tl.sphere(true);
-            const PrimConst pc = tab.pc(i);
-            const float b = 2.0f * dot(mk(pc.ocx, pc.ocy, pc.ocz), d);
-            const float disc = b * b - a4 * pc.c;
-            const float t = a2_ok ? root_t1(b, disc, a2) : root_full(b, disc, a2);
-            if (t > 0.0f && best_s > t) {
-                best_s = t;
-                win_s = i;
-            }
-        };
-        if constexpr (RT_PRIM_BOX && SMAX > 0) {
-            // only the wave's candidate spheres, in ascending order (non-candidates give t <= 0)
-#pragma unroll
-            for (int i = 0; i < SMAX; ++i)
-                if ((pmask >> i) & 1ull) test(i);
-        } else if constexpr (RT_PRIM_BOX) {
-            for (unsigned long long m = pmask; m; m &= m - 1) test((int)__builtin_ctzll(m));
-        } else {
-            for_spheres<SMAX>(p.S, test);
-        }
-    } else {
-        for_spheres<SMAX>(p.S, [&](int i) {
-            tl.sphere(true);
-            const float t = sphere_t(o, d, a2, a4, a2_ok, tab.s(i));
-            if (PRIMARY) {
-                if (t > 0.0f && best_s > t) {
-                    best_s = t;
-                    win_s = i;
-                }
-            } else {
-                const float tm = t - 0.01f;
-                if (tm > 0.0f && tm < best_s) {
-                    best_s = t;
-                    win_s = i;
-                }
-            }
-        });
-    }
+    if (__builtin_amdgcn_ballot_w64(!a2_ok) == 0)  // wave-uniform (the usual case)
+        nearest_spheres<PRIMARY, true>(p, o, d, a2, a4, a2_ok, pmask, best_s, win_s, tl);
+    else
+        nearest_spheres<PRIMARY, false>(p, o, d, a2, a4, a2_ok, pmask, best_s, win_s, tl);
     float best_p = __builtin_inff();
     int win_p = -1;
     for (int i = 0; i < p.P; ++i) {
         tl.plane(true);
-        const float t = plane_t(o, d, p.pl[i]);
-        if (t > 0.0f && t < best_p) {
-            best_p = t;
-            win_p = i;
-        }
+        take_primary(plane_t(o, d, p.pl[i]), i, best_p, win_p);  // t > 0 && t < best (:985-991, :819-821)
     }
     if (best_s < best_p) return Hit{best_s, win_s};
     if (win_p >= 0) return Hit{best_p, ~win_p};
@@ -633,36 +626,31 @@ __device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, const Spher
 #ifndef RT_TERMINAL
 #define RT_TERMINAL 1
 #endif
-template <int SMAX, typename T>
-__device__ __forceinline__ Hit terminal_direct(const LaunchParams& p, const SphereTab<SMAX>& tab, f3 o, f3 d, T& tl) {
+template <typename T>
+__device__ __forceinline__ Hit terminal_direct(const LaunchParams& p, f3 o, f3 d, T& tl) {
     float best_p = __builtin_inff();
     int win_p = -1;
     for (int i = 0; i < p.P; ++i) {
         tl.plane(true);
-        const float t = plane_t(o, d, p.pl[i]);
-        if (t > 0.0f && t < best_p) {
-            best_p = t;
-            win_p = i;
-        }
+        take_primary(plane_t(o, d, p.pl[i]), i, best_p, win_p);
     }
     if (win_p < 0 || !(best_p - 0.01f > 0.0f)) return Hit{0.0f, HIT_NONE};
     const float a = dot(d, d);
     const float a2 = 2.0f * a, a4 = 4.0f * a;
     const bool a2_ok = a2 > 0.0f && a2 < __builtin_inff();
     float best_s = __builtin_inff();
-    for_spheres<SMAX>(p.S, [&](int i) {
-        tl.sphere(true);
-        const float t = sphere_t(o, d, a2, a4, a2_ok, tab.s(i));
-        const float tm = t - 0.01f;
-        if (tm > 0.0f && tm < best_s) best_s = t;
-    });
+    int win_s = -1;
+    if (__builtin_amdgcn_ballot_w64(!a2_ok) == 0)
+        nearest_spheres<false, true>(p, o, d, a2, a4, a2_ok, 0, best_s, win_s, tl);
+    else
+        nearest_spheres<false, false>(p, o, d, a2, a4, a2_ok, 0, best_s, win_s, tl);
     if (best_s < best_p) return Hit{0.0f, HIT_NONE};  // a sphere is selected: Zero
     return Hit{best_p, ~win_p};
 }
 
 // DIRECT kernel: each lane walks its own chain with per-lane (divergent) control flow.
 // STATS: the diagnostic build that also tallies the work actually executed (not timed).
-template <int K, bool GPOW, int SMAX, bool STATS>
+template <int K, bool GPOW, bool STATS>
 __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p) {
     constexpr int LDS_LEVELS = StackFor<K>::lds_levels;  // LdsStack slots, else unused
     __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
@@ -674,7 +662,6 @@ __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p
     const unsigned long long pmask = (RT_PRIM_BOX && p.prim_const) ? prim_box_mask(p, x, y) : 0;
 
     Tally<STATS> tl;
-    const SphereTab<SMAX> tab(p);
     unsigned cnt = 0;  // packed: reflected segments (bits 0-7) | shadow rays << CNT_SHADOW_SHIFT
     if (valid) {
         const f3 cam = mk(p.cam[0], p.cam[1], p.cam[2]);
@@ -691,7 +678,7 @@ __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p
         typename StackFor<K>::type stk(stk_lv, stk_dv);
         stk.origin(d);
         f3 leaf = mk(0.0f, 0.0f, 0.0f);
-        Hit h = nearest_direct<true, SMAX>(p, tab, o, d, tl, pmask);
+        Hit h = nearest_direct<true>(p, o, d, tl, pmask);
         int count = 0;
         for (;;) {
             if (h.prim == HIT_NONE) break;      // nothing hit: plane colour stays Zero
@@ -711,8 +698,7 @@ __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p
             ++count;
             ++cnt;
             // count is the same for every lane still walking: no divergence here
-            h = (RT_TERMINAL && count > p.limit) ? terminal_direct<SMAX>(p, tab, o, d, tl)
-                                                 : nearest_direct<false, SMAX>(p, tab, o, d, tl);
+            h = (RT_TERMINAL && count > p.limit) ? terminal_direct(p, o, d, tl) : nearest_direct<false>(p, o, d, tl);
         }
         // backward fold: every recorded hit is shaded in reverse order; a mirror hit
         // consumes the colour of the segment after it (levels 0..limit push at most one
@@ -723,7 +709,7 @@ __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p
             stk.pop(p, ra, rb);
             const int code = __float_as_int(rb.w);
             const bool is_s = code >= 0;
-            col = shade_direct<GPOW, SMAX>(p, tab, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z),
+            col = shade_direct<GPOW>(p, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z),
                                            mk(rb.x, rb.y, rb.z), ra.w, col, &cnt, tl);
         }
         const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
@@ -965,7 +951,7 @@ __device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d,
                 const float disc = b * b - a4 * pc.c;
                 t = a2_ok ? root_t1(b, disc, a2) : root_full(b, disc, a2);
             } else {
-                t = sphere_t(o, d, a2, a4, a2_ok, p.sph[i]);
+                t = sphere_t<false>(o, d, a2, a4, a2_ok, p.sph[i]);
             }
             if (PRIMARY) {
                 if (t > 0.0f && best_s > t) {
@@ -1061,7 +1047,7 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
                         const int i = base + (int)__builtin_ctzll(mk64);
                         mk64 &= mk64 - 1;
                         tl.sphere(!blocked);
-                        blocked = blocked | shadow_blocked(hs, l, l_ok, p.sph[i]);  // no short-circuit branch
+                        blocked = blocked | shadow_blocked<false>(hs, l, l_ok, p.sph[i]);  // no short-circuit branch
                         if (__builtin_amdgcn_ballot_w64(!blocked) == 0) break;
                     }
                     if (__builtin_amdgcn_ballot_w64(!blocked) == 0) break;
@@ -1220,8 +1206,7 @@ __global__ __launch_bounds__(256) void debug_segments_kernel(LaunchParams p, int
     f3 d = normalize(sub(vp, cam));
     f3 o = cam;
     Tally<false> tl;
-    const SphereTab<0> tab(p);
-    Hit h = nearest_direct<true, 0>(p, tab, o, d, tl, p.S >= 64 ? ~0ull : (1ull << p.S) - 1);  // every sphere
+    Hit h = nearest_direct<true>(p, o, d, tl, p.S >= 64 ? ~0ull : (1ull << p.S) - 1);  // every sphere
     for (int level = 0;; ++level) {
         const bool none = h.prim == HIT_NONE;
         append_segment(out, cap, count, o, add(o, scale(d, none ? 100.0f : h.t)), level == 0 ? 0 : 1,
@@ -1238,7 +1223,7 @@ __global__ __launch_bounds__(256) void debug_segments_kernel(LaunchParams p, int
                 const f3 lp = mk(l.px, l.py, l.pz);
                 float tb = 1.0f;
                 for (int i = 0; i < p.S; ++i) {
-                    if (shadow_blocked(hp, l, l_ok, p.sph[i])) {
+                    if (shadow_blocked<false>(hp, l, l_ok, p.sph[i])) {
                         const f3 oc = sub(hp, mk(p.sph[i].cx, p.sph[i].cy, p.sph[i].cz));
                         const float b = 2.0f * dot(oc, lp);
                         const float c = dot(oc, oc) - p.sph[i].r2;
@@ -1255,7 +1240,7 @@ __global__ __launch_bounds__(256) void debug_segments_kernel(LaunchParams p, int
                                     : mk(p.pl[prim].nx, p.pl[prim].ny, p.pl[prim].nz);
         d = sub(d, scale(normal, 2.0f * dot(d, normal)));
         o = hp;
-        h = nearest_direct<false, 0>(p, tab, o, d, tl);
+        h = nearest_direct<false>(p, o, d, tl);
     }
 }
 
@@ -1308,18 +1293,13 @@ static void launch_by_depth(const LaunchParams& p, dim3 grid, dim3 block, hipStr
     else if (need <= 8) hipLaunchKernelGGL(KERNEL<8>::fn, grid, block, 0, s, p);
     else hipLaunchKernelGGL(KERNEL<64>::fn, grid, block, 0, s, p);
 }
-template <bool GPOW, bool STATS, int SMAX>
+template <bool GPOW, bool STATS>
 struct DirectK {
     template <int K>
     struct at {
-        static constexpr auto fn = trace_direct_kernel<K, GPOW, SMAX, STATS>;
+        static constexpr auto fn = trace_direct_kernel<K, GPOW, STATS>;
     };
 };
-// RT_SREG: scenes with S <= SREG_MAX spheres run the direct kernel with the sphere table in SGPRs
-#ifndef RT_SREG
-#define RT_SREG 0
-#endif
-constexpr int SREG_MAX = 8;
 template <bool GPOW, bool STATS>
 struct BundleK {
     template <int K>
@@ -1331,8 +1311,7 @@ struct BundleK {
 template <bool GPOW, bool STATS>
 static void launch_variant(const LaunchParams& p, bool bundle, dim3 grid, dim3 block, hipStream_t s) {
     if (bundle) launch_by_depth<BundleK<GPOW, STATS>::template at>(p, grid, block, s);
-    else if (RT_SREG && p.S <= SREG_MAX) launch_by_depth<DirectK<GPOW, STATS, SREG_MAX>::template at>(p, grid, block, s);
-    else launch_by_depth<DirectK<GPOW, STATS, 0>::template at>(p, grid, block, s);
+    else launch_by_depth<DirectK<GPOW, STATS>::template at>(p, grid, block, s);
 }
 
 int launch_trace(const LaunchParams& p, bool generic_pow, bool stats, void* stream) {
