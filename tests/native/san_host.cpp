@@ -1,0 +1,233 @@
+// san_host.cpp -- host sanitizer driver for the C ABI's host code (rt_api.cpp), TEST
+// INFRASTRUCTURE ONLY ("host ASan/UBSan build of the oracle and the C ABI").
+//
+// rt_api.cpp is compiled into this translation unit (unity include) with AddressSanitizer +
+// UndefinedBehaviorSanitizer on the host side only (tests/native/Makefile: -Xarch_host), so
+// that the host work that never touches a device can be driven without a GPU:
+//   * scene packing of rt_set_scene (material flags, plane bases, light frames, cull radii,
+//     the even-padded sphere table) on a context with no devices;
+//   * the per-frame view set-up (view_params: camera basis RayTracer.cs:511-523, view plane
+//     :892-896, primary-segment constants, conservative screen boxes in double) over random
+//     and degenerate cameras, cross-checked bit for bit against the oracle's camera view;
+//   * OnKeyPress / OnMouseMove (:543-554, :1058-1061), rt_write_ppm, rt_wire_layout_of,
+//     and the argument checks of every entry point (no device call is reached).
+// Exit status 0 = all checks passed; any sanitizer report aborts the process.
+#include "../../uu-infogr-raytracer_amd/csrc/rt_api.cpp"
+
+#include <cstdint>
+#include <cstdio>
+#include <unistd.h>
+
+#include "../../oracle/oracle.h"
+
+namespace {
+int failures = 0;
+#define CHECK(cond, ...)                                         \
+    do {                                                         \
+        if (!(cond)) {                                           \
+            std::fprintf(stderr, "FAIL %s:%d: ", __FILE__, __LINE__); \
+            std::fprintf(stderr, __VA_ARGS__);                   \
+            std::fputc('\n', stderr);                            \
+            ++failures;                                          \
+        }                                                        \
+    } while (0)
+
+uint64_t rng = 0xC0FFEE5EEDull;
+uint64_t next64() {
+    uint64_t z = (rng += 0x9E3779B97F4A7C15ull);
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+float unif(float lo, float hi) { return lo + (hi - lo) * (float)((next64() >> 40) * (1.0 / 16777216.0)); }
+rt_vec3 v3(float x, float y, float z) { return rt_vec3{x, y, z}; }
+
+bool same_bits(float a, float b) { return std::memcmp(&a, &b, sizeof a) == 0; }
+bool same_vec(rt_vec3 a, rt_vec3 b) { return same_bits(a.x, b.x) && same_bits(a.y, b.y) && same_bits(a.z, b.z); }
+
+rt_material material(int kind) {
+    rt_material m;
+    std::memset(&m, 0, sizeof m);
+    const rt_vec3 c = v3(unif(0, 1), unif(0, 1), unif(0, 1));
+    switch (kind % 5) {
+        case 0: m.kd = m.ka = c; break;
+        case 1: m.kd = m.ka = c, m.ks = v3(0.4f, 0.4f, 0.4f), m.n = 1.0f; break;
+        case 2: m.kd = m.ka = c, m.ks = c, m.n = unif(2.5f, 30.0f); break;  // generic Math.Pow
+        case 3: m.km = v3(1, 1, 1); break;
+        default: m.kd = m.ka = c, m.km = v3(0.5f, 0.5f, 0.5f); break;
+    }
+    return m;
+}
+
+void check_scene_packing() {
+    for (int it = 0; it < 40; ++it) {
+        rt_ctx ctx;  // no devices: rt_set_scene packs on the host and uploads nowhere
+        const int S = it == 0 ? 0 : (int)(next64() % 70), P = (int)(next64() % 4), L = (int)(next64() % 6);
+        std::vector<rt_sphere> sph((size_t)S);
+        std::vector<rt_plane> pl((size_t)P);
+        std::vector<rt_light> li((size_t)L);
+        for (rt_sphere& s : sph) {
+            s.center = v3(unif(-8, 8), unif(-1, 3), unif(2, 40));
+            s.radius = unif(0.0f, 1.5f);
+            s.material = material((int)(next64() % 5));
+        }
+        if (S > 3) sph[3].radius = NAN;
+        for (rt_plane& p : pl) {
+            p.center = v3(unif(-2, 2), unif(-2, 0), unif(0, 50));
+            p.normal = next64() % 5 == 0 ? v3(1, 0, 0) : v3(unif(-1, 1), unif(-1, 1), unif(-1, 1));
+            p.material = material((int)(next64() % 5));
+        }
+        if (P > 1) pl[1].normal = v3(0, 0, 0);
+        for (rt_light& l : li) l.position = v3(unif(-40, 40), unif(-5, 20), unif(-20, 40)), l.intensity = unif(0, 1);
+        if (L > 0 && it % 3 == 0) li[0].position = v3(0, 0, 0);
+        const int limit = (int)(next64() % 64);
+        int rc = rt_set_scene(&ctx, sph.data(), S, pl.data(), P, li.data(), L, v3(0.1f, 0.1f, 0.1f), limit);
+        CHECK(rc == RT_OK, "rt_set_scene rc %d (%s)", rc, ctx.last_error.c_str());
+        const SceneLayout& lay = ctx.layout;
+        CHECK(lay.S == S && lay.P == P && lay.L == L && lay.limit == limit, "layout counts");
+        CHECK(lay.off_mat % 256 == 0 && lay.off_pl % 256 == 0 && lay.off_li % 256 == 0 && lay.off_cull % 256 == 0,
+              "layout alignment");
+        CHECK(lay.off_mat >= sizeof(DevSphere) * (size_t)(S + (S & 1)), "padded sphere table overlaps materials");
+        CHECK(lay.bytes >= lay.off_cull + sizeof(DevSphereCull) * (size_t)S, "cull table outside the blob");
+        CHECK(lay.host_sph.size() == (size_t)S, "host sphere copy");
+        for (int i = 0; i < S; ++i) {
+            const float r2 = sph[(size_t)i].radius * sph[(size_t)i].radius;
+            CHECK(same_bits(lay.host_sph[(size_t)i].r2, r2), "radius^2 of sphere %d", i);
+        }
+        // per-frame view set-up over random, degenerate and far cameras
+        for (int c = 0; c < 25; ++c) {
+            rt_camera cam{v3(unif(-3, 3), unif(-1, 2), unif(-4, 2)), unif(-3.2f, 3.2f), unif(-1.5f, 1.5f)};
+            if (c == 1) cam.position = v3(1e30f, -1e30f, 1e30f);
+            if (c == 2) cam.yaw = NAN;
+            if (c == 3) cam.pitch = INFINITY;
+            if (c == 4 && S > 0) cam.position = sph[0].center;
+            const int W = 1 + (int)(next64() % 4000), H = 1 + (int)(next64() % 2500);
+            rt_set_camera(&ctx, &cam);
+            LaunchParams lp;
+            std::memset(&lp, 0, sizeof lp);
+            rc = view_params(&ctx, W, H, lp);
+            CHECK(rc == RT_OK, "view_params rc %d", rc);
+            CHECK(lp.prim_const == (S <= MAX_PRIM_CONST ? 1 : 0), "prim_const flag");
+            // a box is never empty: the sphere is strictly in front (cz > rho), so both tangent
+            // directions lie in (-pi/2, pi/2) and tan keeps their order
+            for (int i = 0; lp.prim_const && i < S; ++i)
+                CHECK(lp.pbox[i].x0 <= lp.pbox[i].x1 && lp.pbox[i].y0 <= lp.pbox[i].y1,
+                      "empty screen box: sphere %d [%d,%d]x[%d,%d]", i, lp.pbox[i].x0, lp.pbox[i].x1, lp.pbox[i].y0,
+                      lp.pbox[i].y1);
+            rt_view a, b;
+            CHECK(rt_camera_view(&cam, W, H, &a) == RT_OK && oracle_camera_view(&cam, W, H, &b) == RT_OK, "views");
+            CHECK(same_vec(a.right, b.right) && same_vec(a.up, b.up) && same_vec(a.forward, b.forward) &&
+                      same_bits(a.plane_width, b.plane_width) && same_bits(a.plane_height, b.plane_height) &&
+                      same_bits(a.near_clip, b.near_clip),
+                  "rt_camera_view != oracle_camera_view (yaw %a pitch %a %dx%d)", cam.yaw, cam.pitch, W, H);
+        }
+    }
+    rt_ctx ctx;
+    rt_sphere s{};
+    rt_light l{};
+    CHECK(rt_set_scene(&ctx, nullptr, 1, nullptr, 0, nullptr, 0, v3(0, 0, 0), 0) == RT_ERR_INVALID_ARG, "NULL spheres");
+    CHECK(rt_set_scene(&ctx, &s, 1, nullptr, 0, &l, 1, v3(0, 0, 0), -1) == RT_ERR_INVALID_ARG, "negative limit");
+    CHECK(rt_set_scene(&ctx, &s, 1, nullptr, 0, &l, 1, v3(0, 0, 0), RT_MAX_RECURSION_LIMIT + 1) == RT_ERR_UNSUPPORTED,
+          "limit above the stack");
+    CHECK(rt_set_scene(&ctx, &s, 1, nullptr, 0, &l, RT_MAX_LIGHTS + 1, v3(0, 0, 0), 0) == RT_ERR_UNSUPPORTED,
+          "too many lights");
+    // render entry points: argument checks only (the context has no device)
+    int32_t px[4];
+    CHECK(rt_render(nullptr, 2, 2, px) == RT_ERR_INVALID_ARG, "rt_render NULL ctx");
+    CHECK(rt_render_device(&ctx, 2, 2, px, nullptr) == RT_ERR_NO_SCENE, "render before a scene");
+    CHECK(rt_set_scene(&ctx, &s, 1, nullptr, 0, &l, 1, v3(0, 0, 0), 0) == RT_OK, "scene");
+    CHECK(rt_render_device(&ctx, 0, 2, px, nullptr) == RT_ERR_INVALID_ARG, "zero width");
+    CHECK(rt_render_device(&ctx, 65536, 65536, px, nullptr) == RT_ERR_INVALID_ARG, "frame over 2^31 pixels");
+    CHECK(rt_render_bands_ex(&ctx, 8, 8, 0, 0, 1, px, RT_BANDS_INT32, nullptr, nullptr) == RT_ERR_INVALID_ARG,
+          "band_rows 0");
+    CHECK(rt_render_bands_ex(&ctx, 8, 8, 8, 0, 1, px, 7, nullptr, nullptr) == RT_ERR_INVALID_ARG, "bad format");
+    CHECK(rt_render_bands_batch(&ctx, 8, 8, 8, 0, 1, 0, px, 256, RT_BANDS_INT32, nullptr, nullptr) == RT_ERR_INVALID_ARG,
+          "zero frames");
+    CHECK(rt_encode_bands(&ctx, 8, 8, 8, 2, 2, px, 64, 1, px, nullptr, nullptr) == RT_ERR_INVALID_ARG, "rank >= world");
+    CHECK(rt_decode_gathered(&ctx, 8, 8, 8, 2, 0, px, 3, 1, px, 64, nullptr) == RT_ERR_INVALID_ARG, "unaligned stride");
+}
+
+void check_camera_input() {
+    rt_camera c{v3(0, 0, 0), 0, 0};
+    for (int k = 0; k <= 7; ++k) CHECK(rt_camera_on_key(&c, k) == RT_OK, "key %d", k);
+    // W then S at yaw 0: forward (0, -0, 1) * 0.05 out and back
+    rt_camera d{v3(0, 0, 0), 0, 0};
+    rt_camera_on_key(&d, RT_KEY_W);
+    CHECK(same_bits(d.position.z, 0.05f), "W moves along +z by 0.05f");
+    rt_camera_on_key(&d, RT_KEY_S);
+    CHECK(d.position.z == 0.0f, "S undoes W");
+    CHECK(rt_camera_on_mouse_move(&c, 36.0f, -18.0f) == RT_OK, "mouse");
+    CHECK(same_bits(c.yaw, 36.0f / 360.0f) && same_bits(c.pitch, -18.0f / 360.0f), "mouse deltas / 360");
+    CHECK(rt_camera_on_key(nullptr, RT_KEY_W) == RT_ERR_INVALID_ARG, "NULL camera");
+    rt_view v;
+    CHECK(rt_camera_view(&c, 0, 1, &v) == RT_ERR_INVALID_ARG, "zero width view");
+}
+
+void check_ppm() {
+    const int W = 37, H = 5;
+    std::vector<int32_t> px((size_t)W * H);
+    for (size_t i = 0; i < px.size(); ++i) px[i] = (int32_t)(next64() & 0xFFFFFF);
+    char path[] = "/tmp/san_host_XXXXXX";
+    const int fd = mkstemp(path);
+    CHECK(fd >= 0, "mkstemp");
+    if (fd < 0) return;
+    close(fd);
+    CHECK(rt_write_ppm(path, px.data(), W, H) == RT_OK, "rt_write_ppm");
+    FILE* f = std::fopen(path, "rb");
+    std::vector<unsigned char> data(64 + (size_t)W * H * 3);
+    const size_t n = f ? std::fread(data.data(), 1, data.size(), f) : 0;
+    if (f) std::fclose(f);
+    std::remove(path);
+    const char head[] = "P6\n37 5\n255\n";
+    const size_t hl = sizeof head - 1;
+    CHECK(n == hl + (size_t)W * H * 3 && std::memcmp(data.data(), head, hl) == 0, "PPM header/size");
+    for (size_t i = 0; n == hl + (size_t)W * H * 3 && i < px.size(); ++i) {
+        const unsigned char* p = data.data() + hl + 3 * i;
+        CHECK(p[0] == ((px[i] >> 16) & 255) && p[1] == ((px[i] >> 8) & 255) && p[2] == (px[i] & 255), "pixel %zu", i);
+    }
+    CHECK(rt_write_ppm(nullptr, px.data(), W, H) == RT_ERR_INVALID_ARG, "NULL path");
+    CHECK(rt_write_ppm("/nonexistent-dir/x.ppm", px.data(), W, H) != RT_OK, "unwritable path");
+}
+
+void check_wire_layout() {
+    rt_wire_layout lay;
+    for (int it = 0; it < 500; ++it) {
+        const int W = 1 + (int)(next64() % 8192), H = 1 + (int)(next64() % 4400), br = 1 + (int)(next64() % 16);
+        const int world = 1 + (int)(next64() % 9), nf = 1 + (int)(next64() % 128);
+        const int rc = rt_wire_layout_of(W, H, br, world, nf, &lay);
+        if (rc != RT_OK) continue;  // above the codec's 2^26-tile limit
+        const long long rows = (long long)std::max(1, bands_of(H, br, 0, world)) * br;
+        CHECK(lay.tiles_x == (W + 7) / 8 && lay.tiles_y == (int)((rows + 7) / 8), "tile grid");
+        CHECK((long long)lay.n_tiles == (long long)lay.tiles_per_frame * nf && lay.n_chunks == (lay.n_tiles + 7) / 8,
+              "tiles / chunks");
+        CHECK(lay.fixed_bytes % 8 == 0 && lay.max_bytes >= lay.fixed_bytes + 8ull * lay.n_tiles, "wire sizes");
+    }
+    CHECK(rt_wire_layout_of(8192, 8192, 8, 1, 65535, &lay) == RT_ERR_INVALID_ARG, "tile overflow rejected");
+    CHECK(rt_wire_layout_of(8, 8, 8, 0, 1, &lay) == RT_ERR_INVALID_ARG, "world 0");
+    CHECK(rt_wire_layout_of(8, 8, 8, 1, 1, nullptr) == RT_ERR_INVALID_ARG, "NULL layout");
+}
+
+void check_library() {
+    CHECK(rt_abi_version() == RT_ABI_VERSION, "ABI version");
+    int n = -1;
+    CHECK(rt_device_count(&n) == RT_OK && n >= 0, "device count");
+    rt_ctx* ctx = nullptr;
+    CHECK(rt_create_ex(1, 0x100, &ctx) == RT_ERR_INVALID_ARG && !ctx, "unknown flag");
+    CHECK(rt_create(0, &ctx) == RT_ERR_INVALID_ARG, "zero GPUs");
+    if (n == 0) {
+        CHECK(rt_create(1, &ctx) == RT_ERR_NO_DEVICE && !ctx, "no CPU fallback");
+        CHECK(std::strstr(rt_last_error(nullptr), "no HIP device") != nullptr, "last error text");
+    }
+    rt_destroy(nullptr);
+}
+}  // namespace
+
+int main() {
+    check_library();
+    check_scene_packing();
+    check_camera_input();
+    check_ppm();
+    check_wire_layout();
+    std::printf("san_host: %d failures\n", failures);
+    return failures ? 1 : 0;
+}
