@@ -207,6 +207,37 @@ void check_wire_layout() {
     CHECK(rt_wire_layout_of(8, 8, 8, 1, 1, nullptr) == RT_ERR_INVALID_ARG, "NULL layout");
 }
 
+// shadow_threshold: "n >= T" must equal IntersectsSphere's fl(fl(n / a2) - 0.001f) > 0 for every
+// float n, for positive finite a2 -- checked at the threshold's neighbours and at random n.
+bool shadow_ref(float n, float a2) {
+    volatile float q = n / a2;  // correctly rounded binary32 (SSE, no contraction)
+    volatile float d = q - 0.001f;
+    return d > 0.0f;
+}
+void check_shadow_threshold() {
+    long checked = 0;
+    for (int it = 0; it < 200000; ++it) {
+        float a2;
+        switch (it % 4) {
+            case 0: a2 = unif(1.0f, 4.0f); break;                                    // unit-ish directions
+            case 1: a2 = std::ldexp(unif(1.0f, 2.0f), (int)(next64() % 250) - 125); break;
+            case 2: a2 = std::ldexp(unif(1.0f, 2.0f), -126 - (int)(next64() % 23)); break;  // denormal
+            default: { uint32_t u = (uint32_t)(next64() % 0x7F800000u) + 1u; std::memcpy(&a2, &u, 4); }
+        }
+        if (!(a2 > 0.0f) || !(a2 < INFINITY)) continue;
+        const float T = shadow_threshold(a2);
+        float n = T;
+        for (int k = 0; k < 3; ++k) n = std::nextafter(n, -INFINITY);
+        for (int k = 0; k < 7; ++k, n = std::nextafter(n, INFINITY), ++checked)
+            CHECK((n >= T) == shadow_ref(n, a2), "threshold a2=%a n=%a T=%a", a2, n, T);
+        const float r = std::ldexp(unif(-1.0f, 1.0f), (int)(next64() % 60) - 30) * a2;
+        CHECK((r >= T) == shadow_ref(r, a2), "random a2=%a n=%a T=%a", a2, r, T);
+        ++checked;
+    }
+    CHECK(!(NAN >= shadow_threshold(2.0f)) && (INFINITY >= shadow_threshold(2.0f)), "NaN / inf numerators");
+    std::printf("shadow_threshold: %ld (n, 2a) pairs\n", checked);
+}
+
 void check_library() {
     CHECK(rt_abi_version() == RT_ABI_VERSION, "ABI version");
     int n = -1;
@@ -228,6 +259,7 @@ int main() {
     check_camera_input();
     check_ppm();
     check_wire_layout();
+    check_shadow_threshold();
     std::printf("san_host: %d failures\n", failures);
     return failures ? 1 : 0;
 }

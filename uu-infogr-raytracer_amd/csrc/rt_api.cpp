@@ -240,6 +240,29 @@ DevMaterial dev_material(const rt_material& m, rt_vec3 ambient) {
     return d;
 }
 
+// Shadow rays (IntersectShadowLight, RayTracer.cs:573-582 -> IntersectsSphere with epsilon
+// 0.001f, :613-636): with 2a finite and > 0 the ray collides iff fl(fl(n / 2a) - e) > 0, n =
+// fl(-b - sqrt(disc)) (the near root decides, rt_kernel.hip shadow_blocked).  For floats q and
+// e the sign of fl(q - e) is that of q - e, so the test is fl(n / 2a) > e.  Correct rounding is
+// monotonic: fl(z) > e iff z > m, m = e + ulp(e)/2 the midpoint above e, except z == m, which
+// rounds to the even neighbour -- succ(e) when e's significand is odd.  So the collision is
+// n >= m * 2a (odd e) or n > m * 2a (even e); m has 25 significant bits and 2a 24, so the
+// product is exact in double, and for a float n, "n >= T" equals "n >= the smallest float >= T"
+// (and "n > T" equals "n >= the smallest float > T").  Returns that float (+inf above FLT_MAX).
+float shadow_threshold(float a2) {
+    const float e = 0.001f;
+    int ex = 0;
+    (void)std::frexp(e, &ex);                                // e = f * 2^ex, f in [0.5, 1)
+    const double m = (double)e + std::ldexp(1.0, ex - 25);  // + ulp(e) / 2 (ulp = 2^(ex - 24))
+    uint32_t eb;
+    std::memcpy(&eb, &e, sizeof eb);
+    const bool odd = (eb & 1u) != 0;
+    const double T = m * (double)a2;                         // exact
+    float t = (float)T;
+    if ((double)t < T || (!odd && (double)t == T)) t = std::nextafter(t, INFINITY);
+    return t;
+}
+
 int total_bands(int H, int band_rows) { return (H + band_rows - 1) / band_rows; }
 int bands_of(int H, int band_rows, int first, int step) {
     int tb = total_bands(H, band_rows);
@@ -579,6 +602,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
         d.a = hdot(p, p);  // IntersectsSphere's a = Dot(direction, direction), :617
         d.a2 = 2.0f * d.a;
         d.a4 = 4.0f * d.a;
+        d.sh_t = shadow_threshold(d.a2);  // used only when a2 is finite and > 0 (wave-uniform per light)
         // shadow-cull frame (kernel uses it only when a is in [2^-40, 2^40])
         const double len = std::sqrt((double)p.x * p.x + (double)p.y * p.y + (double)p.z * p.z);
         double A[3] = {0.0, 0.0, 1.0};

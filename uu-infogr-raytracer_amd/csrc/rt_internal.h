@@ -47,7 +47,10 @@ struct DevLight {
     float a;      // dot(p, p)       : IntersectsSphere's `a` for a shadow ray (dir = position)
     float a2;     // 2 * a
     float a4;     // 4 * a
-    uint32_t pad0;
+    // Shadow threshold (2a finite and > 0): IntersectsSphere(.., 0.001f) collides iff
+    // fl(-b - sqrt) >= sh_t, i.e. fl(fl(-b - sqrt) / 2a) - 0.001f > 0 without the division
+    // (rt_api.cpp shadow_threshold).
+    float sh_t;
     // shadow-cull frame (culling only, never in a result): A ~ p/|p| (every shadow ray of this
     // light has direction p), U, V ~ orthonormal to A
     float ax, ay, az, pad1;

@@ -34,7 +34,10 @@
 #endif
 
 // One wave (64 lanes, an 8x8 pixel tile) per workgroup: a one-wave group releases its LDS
-// stack slots as soon as it ends (A/B round 1: 2x2-wave groups +8 % on C4).
+// stack slots as soon as it ends.  The dispatcher launches one-wave groups no faster than
+// ~6.9 us per 1080p frame (tools/launch_probe.hip, a store-only kernel), but with real work
+// that is not the limit: 4-wave groups and waves looping over 2/4/8 tiles all measured equal
+// or slower (C2 +0..16 %, C3 +3..22 %, C4 +16..37 %; profiles/ab/r02_tiles_per_wg_rejected.txt).
 constexpr int WG_THREADS = 64, TILE_W = 8, TILE_H = 8;
 
 namespace rtk {
@@ -172,7 +175,12 @@ __device__ __forceinline__ float sphere_t(f3 o, f3 d, float a2, float a4, bool a
 // epsilon 0.001, RayTracer.cs:574-578): collision iff min(max(t1-e,0), max(t2-e,0)) > 0.
 // With 2a finite-positive (uniform per light) and t2 >= t1 that is t1 - e > 0 (and then
 // t2 - e > 0 too); fl(-b - sq) / 2a - e > 0 already implies -b > sq (see root_t1).
-template <bool A2OK>
+// THRESH: the same predicate without the division -- t1 - e > 0 iff fl(-b - sq) >= l.sh_t, the
+// per-light threshold of the correctly rounded quotient (rt_api.cpp shadow_threshold; NaN
+// compares false, as the reference's NaN distance does).  Used by the bundle kernel (C4 -3 % with
+// paired candidates); in the direct kernel the division-free form measured slower (C2 +4 %, C3
+// +6 %: the shading code around it was scheduled worse), so it keeps the division there.
+template <bool A2OK, bool THRESH = false>
 __device__ __forceinline__ bool shadow_blocked(f3 hp, const DevLight& l, bool a2_ok, const DevSphere& s) {
     const f3 oc = sub(hp, mk(s.cx, s.cy, s.cz));
     const float b = 2.0f * dot(oc, mk(l.px, l.py, l.pz));
@@ -182,7 +190,8 @@ __device__ __forceinline__ bool shadow_blocked(f3 hp, const DevLight& l, bool a2
         bool hit = false;
         if (__builtin_amdgcn_ballot_w64(sphere_candidate(b, disc)) != 0) {  // wave-uniform
             const float sq = cr_sqrt(disc);
-            hit = (-b - sq) / l.a2 - 0.001f > 0.0f;
+            if constexpr (THRESH) hit = -b - sq >= l.sh_t;  // == fl(fl(-b - sq) / 2a) - 0.001f > 0
+            else hit = (-b - sq) / l.a2 - 0.001f > 0.0f;
         }
         return hit;
     }
@@ -648,20 +657,17 @@ __device__ __forceinline__ Hit terminal_direct(const LaunchParams& p, f3 o, f3 d
     return Hit{best_p, ~win_p};
 }
 
-// DIRECT kernel: each lane walks its own chain with per-lane (divergent) control flow.
-// STATS: the diagnostic build that also tallies the work actually executed (not timed).
-template <int K, bool GPOW, bool STATS>
-__global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p) {
-    constexpr int LDS_LEVELS = StackFor<K>::lds_levels;  // LdsStack slots, else unused
-    __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
-    __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * WG_THREADS : 1];
+// DIRECT path, one 8x8 tile: each lane walks its own chain with per-lane (divergent) control
+// flow.  Returns the lane's packed counts: reflected segments (bits 0-7) | shadow rays << 8.
+template <int K, bool GPOW, typename T>
+__device__ __forceinline__ unsigned trace_tile_direct(const LaunchParams& p, int tile_x, float2* stk_lv, float* stk_dv,
+                                                      T& tl) {
     const int lane = threadIdx.x & 63;
-    const TilePixel tpx = tile_pixel(p, blockIdx.x * TILE_W + (lane & 7), blockIdx.y * TILE_H + (lane >> 3));
+    const TilePixel tpx = tile_pixel(p, tile_x * TILE_W + (lane & 7), blockIdx.y * TILE_H + (lane >> 3));
     const int x = tpx.x, r = tpx.r, y = tpx.y;
     const bool valid = tpx.valid;
     const unsigned long long pmask = (RT_PRIM_BOX && p.prim_const) ? prim_box_mask(p, x, y) : 0;
 
-    Tally<STATS> tl;
     unsigned cnt = 0;  // packed: reflected segments (bits 0-7) | shadow rays << CNT_SHADOW_SHIFT
     if (valid) {
         const f3 cam = mk(p.cam[0], p.cam[1], p.cam[2]);
@@ -715,8 +721,19 @@ __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p
         const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
         store_pixel(p, r, y, x, px32);
     }
+    return cnt;
+}
 
-    add_counters<STATS>(p, lane, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
+// DIRECT kernel (scenes with < CULL_MIN_SPHERES spheres).
+// STATS: the diagnostic build that also tallies the work actually executed (not timed).
+template <int K, bool GPOW, bool STATS>
+__global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p) {
+    constexpr int LDS_LEVELS = StackFor<K>::lds_levels;  // LdsStack slots, else unused
+    __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
+    __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * WG_THREADS : 1];
+    Tally<STATS> tl;
+    const unsigned cnt = trace_tile_direct<K, GPOW>(p, blockIdx.x, stk_lv, stk_dv, tl);
+    add_counters<STATS>(p, threadIdx.x & 63, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
 }
 
 // ---------------------------------------------------------------------------------
@@ -939,20 +956,17 @@ __device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d,
     for (int base = 0; base < p.S; base += 64) {
         const int n = min(64, p.S - base);
         unsigned long long m = use_box ? pmask : cull_mask(p, B, base, n);  // use_box: S <= 64
-        while (m) {
-            const int i = base + (int)__builtin_ctzll(m);
-            m &= m - 1;
-            tl.sphere(active);
-            float t;
+        auto test = [&](int i) {
             if (PRIMARY && p.prim_const) {
                 // o == camera: oc = cam - c and c = oc.oc - r^2 are per-frame constants (:614-619)
                 const PrimConst pc = p.pc[i];
                 const float b = 2.0f * dot(mk(pc.ocx, pc.ocy, pc.ocz), d);
                 const float disc = b * b - a4 * pc.c;
-                t = a2_ok ? root_t1(b, disc, a2) : root_full(b, disc, a2);
-            } else {
-                t = sphere_t<false>(o, d, a2, a4, a2_ok, p.sph[i]);
+                return a2_ok ? root_t1(b, disc, a2) : root_full(b, disc, a2);
             }
+            return sphere_t<false>(o, d, a2, a4, a2_ok, p.sph[i]);
+        };
+        auto take = [&](float t, int i) {
             if (PRIMARY) {
                 if (t > 0.0f && best_s > t) {
                     best_s = t;
@@ -965,6 +979,13 @@ __device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d,
                     win_s = i;
                 }
             }
+        };
+        // (pairing the candidates as in the shadow loop measured +0.8 % on C4)
+        while (m) {
+            const int i = base + (int)__builtin_ctzll(m);
+            m &= m - 1;
+            tl.sphere(active);
+            take(test(i), i);
         }
     }
     float best_p = __builtin_inff();
@@ -1043,11 +1064,21 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
                 for (int base = 0; base < p.S; base += 64) {
                     const int n = min(64, p.S - base);
                     unsigned long long mk64 = shadow_cull_mask(p, B, l, base, n);
+                    // candidates two at a time: independent tests (ILP across the sqrt chains),
+                    // one pair of sphere loads and one exit ballot per pair; an odd last
+                    // candidate is tested twice (the OR is unchanged)
                     while (mk64) {
-                        const int i = base + (int)__builtin_ctzll(mk64);
+                        const int i0 = base + (int)__builtin_ctzll(mk64);
                         mk64 &= mk64 - 1;
+                        const bool two = mk64 != 0;
+                        const int i1 = two ? base + (int)__builtin_ctzll(mk64) : i0;
+                        if (two) mk64 &= mk64 - 1;
+                        const DevSphere s0 = p.sph[i0], s1 = p.sph[i1];
                         tl.sphere(!blocked);
-                        blocked = blocked | shadow_blocked<false>(hs, l, l_ok, p.sph[i]);  // no short-circuit branch
+                        const bool h0 = shadow_blocked<false, true>(hs, l, l_ok, s0);
+                        tl.sphere(two && !blocked && !h0);
+                        const bool h1 = shadow_blocked<false, true>(hs, l, l_ok, s1);
+                        blocked = blocked | h0 | h1;  // no short-circuit branch
                         if (__builtin_amdgcn_ballot_w64(!blocked) == 0) break;
                     }
                     if (__builtin_amdgcn_ballot_w64(!blocked) == 0) break;
@@ -1070,17 +1101,14 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
 
 // BUNDLE kernel (scenes with >= CULL_MIN_SPHERES spheres): converged control flow so that
 // every segment and every light can form a wave bundle and cull the sphere list.
-template <int K, bool GPOW, bool STATS>
-__global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel(LaunchParams p) {
-    constexpr int LDS_LEVELS = StackFor<K>::lds_levels;  // LdsStack slots, else unused
-    __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
-    __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * WG_THREADS : 1];
+template <int K, bool GPOW, typename T>
+__device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int tile_x, float2* stk_lv, float* stk_dv,
+                                                      T& tl) {
     const int lane = threadIdx.x & 63;
-    const TilePixel tpx = tile_pixel(p, blockIdx.x * TILE_W + (lane & 7), blockIdx.y * TILE_H + (lane >> 3));
+    const TilePixel tpx = tile_pixel(p, tile_x * TILE_W + (lane & 7), blockIdx.y * TILE_H + (lane >> 3));
     const int x = tpx.x, r = tpx.r, y = tpx.y;
     const bool valid = tpx.valid;
 
-    Tally<STATS> tl;
     unsigned cnt = 0;  // packed: reflected segments (bits 0-7) | shadow rays << CNT_SHADOW_SHIFT
     const f3 cam = mk(p.cam[0], p.cam[1], p.cam[2]);
     // TracePixel primary ray, :963-971 (no half-pixel offset)
@@ -1178,8 +1206,17 @@ __global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel(LaunchParams p
         const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
         store_pixel(p, r, y, x, px32);
     }
+    return cnt;
+}
 
-    add_counters<STATS>(p, lane, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
+template <int K, bool GPOW, bool STATS>
+__global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel(LaunchParams p) {
+    constexpr int LDS_LEVELS = StackFor<K>::lds_levels;  // LdsStack slots, else unused
+    __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
+    __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * WG_THREADS : 1];
+    Tally<STATS> tl;
+    const unsigned cnt = trace_tile_bundle<K, GPOW>(p, blockIdx.x, stk_lv, stk_dv, tl);
+    add_counters<STATS>(p, threadIdx.x & 63, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
 }
 
 // ---------------------------------------------------------------------------------
