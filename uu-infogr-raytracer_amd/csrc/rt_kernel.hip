@@ -356,14 +356,18 @@ constexpr unsigned CNT_REFL_MASK = 0xFFu;
 // sphere loop ran (a shadow ray is skipped when its outcome cannot change the pixel, and culling
 // skips sphere tests that provably cannot select) -- reported beside the nominal counts of
 // SURVEY.md 8(d), which count every primitive of every ray.
-template <bool ON>
+// SMAX > 0: the scene has at most SMAX spheres (a compile-time bound: the pair loops over the
+// sphere table are unrolled, no loop counter or pointer arithmetic on the scalar unit).
+template <bool ON, int SMAX = 0>
 struct Tally {
+    static constexpr int smax = SMAX;
     __device__ __forceinline__ void sphere(bool) {}
     __device__ __forceinline__ void plane(bool) {}
     __device__ __forceinline__ void shadow(bool) {}
 };
-template <>
-struct Tally<true> {
+template <int SMAX>
+struct Tally<true, SMAX> {
+    static constexpr int smax = SMAX;
     unsigned s = 0, pl = 0, sh = 0;
     __device__ __forceinline__ void sphere(bool c) { s += c ? 1u : 0u; }
     __device__ __forceinline__ void plane(bool c) { pl += c ? 1u : 0u; }
@@ -376,9 +380,9 @@ struct Tally<true> {
 // LaunchParams, so its counts are identical: frame 0 counts for all n_frames of them -- one
 // atomic pair per wave per launch instead of per frame (each device-scope atomic is a memory
 // round trip on MI355X, 32 B of HBM write traffic).
-template <bool ST>
+template <bool ST, int SM>
 __device__ __forceinline__ void add_counters(const LaunchParams& p, int lane, unsigned n_refl, unsigned n_shadow,
-                                             const Tally<ST>& tl) {
+                                             const Tally<ST, SM>& tl) {
     if (blockIdx.z != 0) return;  // wave-uniform
     const unsigned long long nf = p.n_frames > 1 ? (unsigned long long)p.n_frames : 1ull;
     const unsigned b = wave_count(n_refl), c = wave_count(n_shadow);
@@ -443,25 +447,39 @@ __device__ __forceinline__ bool shadow_matters(f3 ph, float intensity, float att
     return !(finite && zero_or_nan(ph.x) && zero_or_nan(ph.y) && zero_or_nan(ph.z));
 }
 
-// IntersectShadowLight's sphere loop (:577-579) for the active lanes: a wave-uniform loop over
-// pairs of spheres that ends when every active lane is blocked (the reference's loop has no
-// early exit, but a blocked ray stays blocked).  A lane's result is the OR of its tests, as in
-// the reference.  The scalar unit bounds these kernels (one per CU for 4 SIMDs,
-// profiles/r02_issue_probe.txt), so the loop is shaped for scalar economy: the blocked state is
-// a VGPR value (no lane-mask phi), one 32-byte scalar load and one exit ballot per pair (the
-// device table is padded to an even count with a sphere that never hits, rt_set_scene), no
-// per-lane loop exits (their mask bookkeeping cost ~28 scalar instructions per sphere).
+// Loop over the sphere table two spheres at a time (the device table is padded to an even count
+// with a sphere that never hits, rt_set_scene): body(i) tests spheres i and i + 1.  Unrolled
+// when the scene's sphere count has a compile-time bound (T::smax).
+template <typename T, typename F>
+__device__ __forceinline__ void for_sphere_pairs(const LaunchParams& p, F body) {
+    if constexpr (T::smax > 0) {
+#pragma unroll
+        for (int i = 0; i < T::smax; i += 2) {
+            if (i >= p.S) break;  // wave-uniform
+            body(i);
+        }
+    } else {
+        for (int i = 0; i < p.S; i += 2) body(i);
+    }
+}
+
+// IntersectShadowLight's sphere loop (:577-579) for the active lanes: every sphere, a lane's
+// result the OR of its tests, as in the reference.  The scalar unit bounds these kernels (one per
+// CU for 4 SIMDs, profiles/r02_issue_probe.txt), so the loop is shaped for scalar economy: the
+// blocked state is a VGPR value (no lane-mask phi), one 32-byte scalar load per pair, no per-lane
+// loop exits (their mask bookkeeping cost ~28 scalar instructions per sphere) and no wave exit
+// once every lane is blocked (it almost never fires: C2 -1.4 %, C3 -1.0 % without it,
+// profiles/ab/r02_shadow_loop.txt).
 template <bool A2OK, typename T>
 __device__ __forceinline__ bool shadow_scan(const LaunchParams& p, f3 hp, const DevLight& l, T& tl) {
     int blk = 0;
-    for (int i = 0; i < p.S; i += 2) {
+    for_sphere_pairs<T>(p, [&](int i) {
         const DevSphere s0 = p.sph[i], s1 = p.sph[i + 1];
         tl.sphere(blk == 0);
         blk = shadow_blocked<A2OK>(hp, l, false, s0) ? 1 : blk;
         tl.sphere((blk == 0) & (i + 1 < p.S));
         blk = shadow_blocked<A2OK>(hp, l, false, s1) ? 1 : blk;
-        if (__builtin_amdgcn_ballot_w64(blk == 0) == 0) break;
-    }
+    });
     return blk != 0;
 }
 
@@ -587,7 +605,7 @@ __device__ __forceinline__ void nearest_spheres(const LaunchParams& p, f3 o, f3 
         }
     } else {
         // pairs (the device table is padded to an even count with a sphere that never hits)
-        for (int i = 0; i < p.S; i += 2) {
+        for_sphere_pairs<T>(p, [&](int i) {
             const DevSphere s0 = p.sph[i], s1 = p.sph[i + 1];
             tl.sphere(true);
             tl.sphere(i + 1 < p.S);
@@ -600,7 +618,7 @@ __device__ __forceinline__ void nearest_spheres(const LaunchParams& p, f3 o, f3 
                 take_secondary(t0, i, best_s, win_s);
                 take_secondary(t1, i + 1, best_s, win_s);
             }
-        }
+        });
     }
 }
 
@@ -669,6 +687,8 @@ __device__ __forceinline__ unsigned trace_tile_direct(const LaunchParams& p, int
     const unsigned long long pmask = (RT_PRIM_BOX && p.prim_const) ? prim_box_mask(p, x, y) : 0;
 
     unsigned cnt = 0;  // packed: reflected segments (bits 0-7) | shadow rays << CNT_SHADOW_SHIFT
+    typename StackFor<K>::type stk(stk_lv, stk_dv);
+    f3 leaf = mk(0.0f, 0.0f, 0.0f);
     if (valid) {
         const f3 cam = mk(p.cam[0], p.cam[1], p.cam[2]);
         // TracePixel primary ray, :963-971 (no half-pixel offset)
@@ -681,9 +701,7 @@ __device__ __forceinline__ unsigned trace_tile_direct(const LaunchParams& p, int
         f3 d = normalize(sub(vp, cam));
         f3 o = cam;
 
-        typename StackFor<K>::type stk(stk_lv, stk_dv);
         stk.origin(d);
-        f3 leaf = mk(0.0f, 0.0f, 0.0f);
         Hit h = nearest_direct<true>(p, o, d, tl, pmask);
         int count = 0;
         for (;;) {
@@ -708,7 +726,9 @@ __device__ __forceinline__ unsigned trace_tile_direct(const LaunchParams& p, int
         }
         // backward fold: every recorded hit is shaded in reverse order; a mirror hit
         // consumes the colour of the segment after it (levels 0..limit push at most one
-        // record each, so K = limit + 1 records suffice)
+        // record each, so K = limit + 1 records suffice).  Per lane, divergent: the bundle
+        // kernel's converged fold with wave-level shadow culling measured slower here (C2
+        // +14 %, C3 +17 %, profiles/ab/r02_direct_converged_fold_rejected.txt)
         f3 col = leaf;
         while (stk.n > 0) {
             float4 ra, rb;
@@ -726,12 +746,12 @@ __device__ __forceinline__ unsigned trace_tile_direct(const LaunchParams& p, int
 
 // DIRECT kernel (scenes with < CULL_MIN_SPHERES spheres).
 // STATS: the diagnostic build that also tallies the work actually executed (not timed).
-template <int K, bool GPOW, bool STATS>
+template <int K, bool GPOW, bool STATS, int SMAX>
 __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p) {
     constexpr int LDS_LEVELS = StackFor<K>::lds_levels;  // LdsStack slots, else unused
     __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
     __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * WG_THREADS : 1];
-    Tally<STATS> tl;
+    Tally<STATS, SMAX> tl;
     const unsigned cnt = trace_tile_direct<K, GPOW>(p, blockIdx.x, stk_lv, stk_dv, tl);
     add_counters<STATS>(p, threadIdx.x & 63, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
 }
@@ -1099,6 +1119,38 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
     return act ? col : sec;
 }
 
+// Backward fold (converged call, all 64 lanes): level by level from the deepest, every recorded
+// hit is shaded; a mirror hit consumes the colour of the segment after it (levels 0..limit push
+// at most one record each, so K = limit + 1 records suffice).  Returns the lane's colour.
+template <bool GPOW, typename STK, typename T>
+__device__ __forceinline__ f3 fold_converged(const LaunchParams& p, STK& stk, f3 leaf, unsigned* cnt, T& tl) {
+    f3 col = leaf;
+    const int depth = stk.n;
+    int level = (int)wave_max((float)depth);
+    while (level-- > 0) {
+        const bool act = level < depth;  // this lane's top record is at `level`
+        float4 ra = make_float4(0.0f, 0.0f, 0.0f, 1.0f), rb = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
+        if (act) stk.pop(p, ra, rb);
+        const unsigned long long am = __builtin_amdgcn_ballot_w64(act);
+        if (am != ~0ull) {  // idle lanes shade a copy of the first active lane's record
+            const int ref = __builtin_ctzll(am);
+            const float4 qa = make_float4(readlane_f(ra.x, ref), readlane_f(ra.y, ref), readlane_f(ra.z, ref),
+                                          readlane_f(ra.w, ref));
+            const float4 qb = make_float4(readlane_f(rb.x, ref), readlane_f(rb.y, ref), readlane_f(rb.z, ref),
+                                          readlane_f(rb.w, ref));
+            if (!act) {
+                ra = qa;
+                rb = qb;
+            }
+        }
+        const int code = __float_as_int(rb.w);
+        const bool is_s = code >= 0;
+        col = shade_bundle<GPOW>(p, act, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z), ra.w,
+                                 col, cnt, tl);
+    }
+    return col;
+}
+
 // BUNDLE kernel (scenes with >= CULL_MIN_SPHERES spheres): converged control flow so that
 // every segment and every light can form a wave bundle and cull the sphere list.
 template <int K, bool GPOW, typename T>
@@ -1175,33 +1227,7 @@ __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int
         }
     }
 
-    // backward fold (converged): level by level from the deepest, every recorded hit is
-    // shaded; a mirror hit consumes the colour of the segment after it (levels 0..limit
-    // push at most one record each, so K = limit + 1 records suffice)
-    f3 col = leaf;
-    const int depth = stk.n;
-    int level = (int)wave_max((float)depth);
-    while (level-- > 0) {
-        const bool act = level < depth;  // this lane's top record is at `level`
-        float4 ra = make_float4(0.0f, 0.0f, 0.0f, 1.0f), rb = make_float4(0.0f, 0.0f, 1.0f, 0.0f);
-        if (act) stk.pop(p, ra, rb);
-        const unsigned long long am = __builtin_amdgcn_ballot_w64(act);
-        if (am != ~0ull) {  // idle lanes shade a copy of the first active lane's record
-            const int ref = __builtin_ctzll(am);
-            const float4 qa = make_float4(readlane_f(ra.x, ref), readlane_f(ra.y, ref), readlane_f(ra.z, ref),
-                                          readlane_f(ra.w, ref));
-            const float4 qb = make_float4(readlane_f(rb.x, ref), readlane_f(rb.y, ref), readlane_f(rb.z, ref),
-                                          readlane_f(rb.w, ref));
-            if (!act) {
-                ra = qa;
-                rb = qb;
-            }
-        }
-        const int code = __float_as_int(rb.w);
-        const bool is_s = code >= 0;
-        col = shade_bundle<GPOW>(p, act, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z), ra.w,
-                                 col, &cnt, tl);
-    }
+    const f3 col = fold_converged<GPOW>(p, stk, leaf, &cnt, tl);
     if (valid) {
         const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
         store_pixel(p, r, y, x, px32);
@@ -1330,11 +1356,11 @@ static void launch_by_depth(const LaunchParams& p, dim3 grid, dim3 block, hipStr
     else if (need <= 8) hipLaunchKernelGGL(KERNEL<8>::fn, grid, block, 0, s, p);
     else hipLaunchKernelGGL(KERNEL<64>::fn, grid, block, 0, s, p);
 }
-template <bool GPOW, bool STATS>
+template <bool GPOW, bool STATS, int SMAX>
 struct DirectK {
     template <int K>
     struct at {
-        static constexpr auto fn = trace_direct_kernel<K, GPOW, STATS>;
+        static constexpr auto fn = trace_direct_kernel<K, GPOW, STATS, SMAX>;
     };
 };
 template <bool GPOW, bool STATS>
@@ -1345,10 +1371,18 @@ struct BundleK {
     };
 };
 
+// Scenes with at most DIRECT_SMAX spheres (every BASELINE config of the direct kernel) run a
+// direct kernel whose sphere-pair loops are unrolled.
+#ifndef RT_DIRECT_SMAX
+#define RT_DIRECT_SMAX 8
+#endif
+constexpr int DIRECT_SMAX = RT_DIRECT_SMAX;
+
 template <bool GPOW, bool STATS>
 static void launch_variant(const LaunchParams& p, bool bundle, dim3 grid, dim3 block, hipStream_t s) {
     if (bundle) launch_by_depth<BundleK<GPOW, STATS>::template at>(p, grid, block, s);
-    else launch_by_depth<DirectK<GPOW, STATS>::template at>(p, grid, block, s);
+    else if (p.S <= DIRECT_SMAX) launch_by_depth<DirectK<GPOW, STATS, DIRECT_SMAX>::template at>(p, grid, block, s);
+    else launch_by_depth<DirectK<GPOW, STATS, 0>::template at>(p, grid, block, s);
 }
 
 int launch_trace(const LaunchParams& p, bool generic_pow, bool stats, void* stream) {
