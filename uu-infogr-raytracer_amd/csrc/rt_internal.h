@@ -6,7 +6,7 @@
 //   DevSphere  [S]   {center.xyz, radius^2}                 16 B   intersection loops
 //   DevMaterial[S+P] sphere materials then plane materials  64 B   shading (per-lane gather)
 //   DevPlane   [P]   {center, c.n, normal, e1, e2}          64 B
-//   DevLight   [L]   {position, intensity, |p|^2 terms}     32 B
+//   DevLight   [L]   {position, intensity, |p|^2 terms, shadow threshold, cull frame}  64 B
 // Everything that the reference recomputes per call but that depends only on scene
 // constants (radius^2 :336, dot(center,normal) :594, checkerboard basis e1/e2 :760-765,
 // ambient*Ka :778/:873, dot(light,light) for the shadow ray :617) is computed once on the
@@ -88,11 +88,9 @@ struct PrimConst {
 };
 constexpr int MAX_PRIM_CONST = 64;
 
-// Scenes with at least this many spheres use wave-bundle culling (rt_kernel.hip).
-#ifndef RT_CULL_MIN
-#define RT_CULL_MIN 12
-#endif
-constexpr int CULL_MIN_SPHERES = RT_CULL_MIN;
+// Scenes with at least this many spheres use wave-bundle culling (rt_kernel.hip; the bundle
+// kernel on the 8-sphere configs measured +20 %, profiles/ab/r02_direct_converged_fold_rejected.txt).
+constexpr int CULL_MIN_SPHERES = 12;
 
 
 // Per-launch parameters (passed by value as the kernel argument block, < 4 KiB).

@@ -26,13 +26,6 @@
 #include "rt_fastmath.h"
 #include "rt_internal.h"
 
-// RT_FASTMATH 1 (shipped): correctly rounded sqrt / reciprocal / division through the short
-// sequences of rt_fastmath.h inside their verified domains (same bits as the generic
-// operations for every input, tools/fastmath_check.hip); 0 = the generic sequences.
-#ifndef RT_FASTMATH
-#define RT_FASTMATH 1
-#endif
-
 // One wave (64 lanes, an 8x8 pixel tile) per workgroup: a one-wave group releases its LDS
 // stack slots as soon as it ends.  The dispatcher launches one-wave groups no faster than
 // ~6.9 us per 1080p frame (tools/launch_probe.hip, a store-only kernel), but with real work
@@ -42,32 +35,13 @@ constexpr int WG_THREADS = 64, TILE_W = 8, TILE_H = 8;
 
 namespace rtk {
 
-// Correctly rounded binary32 operations (bit-identical either way, see rt_fastmath.h).
-// RT_FASTMATH bits: 1 = normalize's 1/sqrt, 2 = other sqrt, 4 = reciprocal / division.
-__device__ __forceinline__ float cr_sqrt(float x) {
-    if constexpr ((RT_FASTMATH & 2) != 0) return sqrt_cr(x);
-    else return __builtin_sqrtf(x);
-}
-__device__ __forceinline__ float cr_inv_len(float x) {  // 1f / MathF.Sqrt(x)
-    if constexpr ((RT_FASTMATH & 1) != 0) return inv_len_cr(x);
-    else return 1.0f / __builtin_sqrtf(x);
-}
-__device__ __forceinline__ float cr_rcp(float x) {
-    if constexpr ((RT_FASTMATH & 4) != 0) return rcp_cr(x);
-    else return 1.0f / x;
-}
-// a / b where the quotient is used only when `need` (the generic fallback runs only there).
-__device__ __forceinline__ float cr_div_if(bool need, float a, float b) {
-    if constexpr ((RT_FASTMATH & 4) != 0) {
-        float q = div_cr_fast(a, b);
-        if (__builtin_expect(need && !(fm_in(a, FM_DIV_LO, FM_DIV_HI) && fm_in(b, FM_DIV_LO, FM_DIV_HI)), 0))
-            q = a / b;
-        return q;
-    } else {
-        (void)need;
-        return a / b;
-    }
-}
+// Correctly rounded binary32 operations.  Vector3.Normalize's 1f / MathF.Sqrt(x) runs the short
+// sequence of rt_fastmath.h inside its verified domain (the same bits as the generic sequence for
+// every input, tools/fastmath_check.hip); the same treatment of the other sqrt and of division
+// measured slower (profiles/ab/r01_fastmath.txt), so they use the generic operations.
+__device__ __forceinline__ float cr_sqrt(float x) { return __builtin_sqrtf(x); }
+__device__ __forceinline__ float cr_inv_len(float x) { return inv_len_cr(x); }  // 1f / MathF.Sqrt(x)
+__device__ __forceinline__ float cr_rcp(float x) { return 1.0f / x; }
 
 struct f3 {
     float x, y, z;
@@ -434,14 +408,10 @@ __device__ __forceinline__ void take_secondary(float t, int i, float& best, int&
 // A light's shadow test can change the pixel only through I * att * phong vs 0 * phong.  When
 // every phong component is +-0 or NaN and I * att is finite, both give +-0 / NaN per
 // component (the sign of a zero never reaches a pixel: only additions, products, IEEE max and
-// the final clamp follow), so the test is skipped (RT_SHADOW_SKIP).  Ray counters are unchanged
+// the final clamp follow), so the test is skipped.  Ray counters are unchanged
 // (shadow rays = shaded diffuse hits x lights); the diagnostic tally counts the tests that ran.
-#ifndef RT_SHADOW_SKIP
-#define RT_SHADOW_SKIP 1
-#endif
 __device__ __forceinline__ bool zero_or_nan(float v) { return !(v != 0.0f && v == v); }
 __device__ __forceinline__ bool shadow_matters(f3 ph, float intensity, float att) {
-    if constexpr (!RT_SHADOW_SKIP) return true;
     const float ia = intensity * att;
     const bool finite = __builtin_fabsf(ia) < __builtin_inff();
     return !(finite && zero_or_nan(ph.x) && zero_or_nan(ph.y) && zero_or_nan(ph.z));
@@ -545,9 +515,6 @@ __device__ __forceinline__ f3 shade_direct(const LaunchParams& p, bool is_sphere
 // mapping is monotonic).  The wave's start has no dependent chain of memory round trips: the
 // box is one unconditional 16-byte load (lane 0's for lanes >= S), tested without
 // short-circuit branches.  Converged call; p.prim_const required.
-#ifndef RT_PRIM_BOX
-#define RT_PRIM_BOX 1
-#endif
 __device__ __forceinline__ unsigned long long prim_box_mask(const LaunchParams& p, int x, int y) {
     const int x_lo = __builtin_amdgcn_readlane(x, 0), x_hi = __builtin_amdgcn_readlane(x, 63);
     const int y_lo = __builtin_amdgcn_readlane(y, 0), y_hi = __builtin_amdgcn_readlane(y, 63);
@@ -593,7 +560,7 @@ __device__ __forceinline__ void nearest_spheres(const LaunchParams& p, f3 o, f3 
     if (PRIMARY && p.prim_const) {
         // o == camera: oc = cam - c and c = oc.oc - r^2 are the same per frame (:614-619);
         // only the wave's candidate spheres, in ascending order (non-candidates give t <= 0)
-        for (unsigned long long m = RT_PRIM_BOX ? pmask : (p.S >= 64 ? ~0ull : (1ull << p.S) - 1); m;) {
+        for (unsigned long long m = pmask; m;) {
             const int i = (int)__builtin_ctzll(m);
             m &= ~(1ull << i);
             tl.sphere(true);
@@ -648,11 +615,8 @@ __device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d,
 // selected with t - 0.01 > 0 and no sphere beats it (TraceSecondaryRay :789-826 with the
 // terminal colours of TracePlane :734 / TraceSphere :843), otherwise Zero.  Planes first:
 // with no plane hit, or the nearest within 0.01, the colour is Zero whatever the spheres do,
-// so they are not tested (RT_TERMINAL).  Returns HIT_NONE (Zero) or the plane hit (One);
+// so they are not tested.  Returns HIT_NONE (Zero) or the plane hit (One);
 // the walk classifies it exactly as it would the full nearest hit.
-#ifndef RT_TERMINAL
-#define RT_TERMINAL 1
-#endif
 template <typename T>
 __device__ __forceinline__ Hit terminal_direct(const LaunchParams& p, f3 o, f3 d, T& tl) {
     float best_p = __builtin_inff();
@@ -684,7 +648,7 @@ __device__ __forceinline__ unsigned trace_tile_direct(const LaunchParams& p, int
     const TilePixel tpx = tile_pixel(p, tile_x * TILE_W + (lane & 7), blockIdx.y * TILE_H + (lane >> 3));
     const int x = tpx.x, r = tpx.r, y = tpx.y;
     const bool valid = tpx.valid;
-    const unsigned long long pmask = (RT_PRIM_BOX && p.prim_const) ? prim_box_mask(p, x, y) : 0;
+    const unsigned long long pmask = p.prim_const ? prim_box_mask(p, x, y) : 0;
 
     unsigned cnt = 0;  // packed: reflected segments (bits 0-7) | shadow rays << CNT_SHADOW_SHIFT
     typename StackFor<K>::type stk(stk_lv, stk_dv);
@@ -722,7 +686,7 @@ __device__ __forceinline__ unsigned trace_tile_direct(const LaunchParams& p, int
             ++count;
             ++cnt;
             // count is the same for every lane still walking: no divergence here
-            h = (RT_TERMINAL && count > p.limit) ? terminal_direct(p, o, d, tl) : nearest_direct<false>(p, o, d, tl);
+            h = count > p.limit ? terminal_direct(p, o, d, tl) : nearest_direct<false>(p, o, d, tl);
         }
         // backward fold: every recorded hit is shaded in reverse order; a mirror hit
         // consumes the colour of the segment after it (levels 0..limit push at most one
@@ -957,7 +921,7 @@ __device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d,
     const unsigned long long am = __builtin_amdgcn_ballot_w64(active);
     if (am == 0) return Hit{0.0f, HIT_NONE};
     // primary segment: the per-frame screen boxes replace the bundle cull
-    const bool use_box = PRIMARY && RT_PRIM_BOX && p.prim_const;
+    const bool use_box = PRIMARY && p.prim_const;
     Bundle B{};
     if (!use_box) B = make_bundle(o, d, active, false);
     if (am != ~0ull) {  // idle lanes trace an exact copy of the first active lane's ray, so
@@ -1178,7 +1142,7 @@ __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int
     stk.origin(d);
     f3 leaf = mk(0.0f, 0.0f, 0.0f);
     bool active = valid;
-    const unsigned long long pmask = (RT_PRIM_BOX && p.prim_const) ? prim_box_mask(p, x, y) : 0;
+    const unsigned long long pmask = p.prim_const ? prim_box_mask(p, x, y) : 0;
     Hit h = nearest_bundle<true>(p, o, d, active, tl, pmask);
     for (int count = 0;; ++count) {
         if (active) {
@@ -1202,7 +1166,7 @@ __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int
             }
         }
         if (__builtin_amdgcn_ballot_w64(active) == 0) break;
-        if (RT_TERMINAL && count + 1 > p.limit) {
+        if (count + 1 > p.limit) {
             // terminal segment (see terminal_direct): only lanes whose nearest plane lies beyond
             // 0.01 need the spheres; the others are Zero
             float best_p = __builtin_inff();
@@ -1373,10 +1337,7 @@ struct BundleK {
 
 // Scenes with at most DIRECT_SMAX spheres (every BASELINE config of the direct kernel) run a
 // direct kernel whose sphere-pair loops are unrolled.
-#ifndef RT_DIRECT_SMAX
-#define RT_DIRECT_SMAX 8
-#endif
-constexpr int DIRECT_SMAX = RT_DIRECT_SMAX;
+constexpr int DIRECT_SMAX = 8;
 
 template <bool GPOW, bool STATS>
 static void launch_variant(const LaunchParams& p, bool bundle, dim3 grid, dim3 block, hipStream_t s) {
