@@ -88,6 +88,11 @@ def parse(argv=None):
                     help="N>1 path: after the timed run rank 0 compares every frame still in its frame rings (tiles) "
                          "with a single-launch render of the same view; exit 3 on a mismatch")
     ap.add_argument("--master-port", type=int, default=29531, help="self-launch (--gpus N > 1): rendezvous port")
+    ap.add_argument("--rehearse-gloo", action="store_true",
+                    help="rehearsal of the N > 1 path on fewer GPUs than ranks: the N ranks share the visible GPUs "
+                         "(rank r on device r %% count) and the collectives run over gloo (RCCL refuses two ranks on "
+                         "one GPU).  Exercises every rank's code path (bands, codec, pipelined gathers, compositor, "
+                         "barrier and max-over-ranks timing); the line is marked 'rehearsal' and is not a result")
     ap.add_argument("--cpu-seconds", type=float, default=20.0,
                     help="CPU baseline budget: about half on the bench config, the rest on C1 and the verbatim "
                          "reference scene")
@@ -296,7 +301,7 @@ def main():
         sys.exit(2)
     if action == "spawn":
         n = device_count()
-        if n < args.gpus:
+        if n < args.gpus and not (args.rehearse_gloo and n >= 1):
             print(f"bench.py --gpus {args.gpus}: only {n} GPU(s) visible", file=sys.stderr, flush=True)
             sys.exit(2)
         sys.exit(subprocess.call(launch_command(sys.argv[1:], args.gpus, args.master_port)))
@@ -316,10 +321,16 @@ def main():
         return main_single(args, torch, Context, abi, scenes)
 
     # N > 1 (or the one-process rehearsal of that path): one process per GPU, RCCL process group
+    # (--rehearse-gloo: the ranks share the visible GPUs and talk over gloo)
+    if args.rehearse_gloo:
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29531")
-    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
+    if args.rehearse_gloo:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    else:
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
     if args.band_format == "tiles" and not args.no_pipeline and args.inflight > 2:
         # the next-but-one batch reuses raw[b % 2]: with a third trace stream it could overwrite the
         # band set that encode(b) still reads
@@ -594,6 +605,9 @@ def main():
             # the loop, e.g. the N>1 pipeline's size handshake): ~ms_per_step when host-bound
             "host_ms_per_step": host_s * 1e3,
         }
+        if args.rehearse_gloo:
+            out["rehearsal"] = (f"gloo: {world} ranks sharing {torch.cuda.device_count()} GPU(s) -- a check of the N > 1 "
+                                f"code path, not a measurement")
         if tg is not None:
             # wire bytes each rank shipped per frame (max over ranks, as gathered), vs the raw band set
             out["config"]["gather_wire_bytes_per_frame"] = tg.bytes_sent / steps

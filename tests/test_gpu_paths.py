@@ -151,3 +151,23 @@ def test_tile_pipeline_on_cuda_streams(extra):
     import json
     line = json.loads(r.stdout.strip().splitlines()[-1])
     assert line["verified_frames"] >= 16 and line["n_gpus"] == 1
+
+
+@pytest.mark.parametrize("world,extra", [(2, ["--compositor", "auto"]), (3, ["--compositor", "on"])])
+def test_bench_multi_rank_rehearsal(world, extra):
+    """bench.py --gpus N as N processes (started by bench.py itself through torch.distributed.run)
+    sharing this GPU, collectives over gloo (--rehearse-gloo: RCCL refuses two ranks on one GPU):
+    every rank's N > 1 code path -- its bands, the tile codec, the pipelined size reduce and
+    gather, rank 0's decode (or compositor mode), the barrier and max-over-ranks timing -- with
+    rank 0's frames checked against a single-launch render (--verify)."""
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--rehearse-gloo",
+           "--master-port", str(_free_port()), "--config", "C3", "--size", "640x360", "--steps", "48", "--warmup", "16",
+           "--batch", "8", "--verify", "--no-cpu-baseline"] + extra
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    import json
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert line["n_gpus"] == world and line["verified_frames"] >= 16 and "rehearsal" in line

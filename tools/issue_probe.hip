@@ -26,7 +26,7 @@
 
 constexpr int ITERS = 4096;
 
-template <int MODE>  // 0 salu, 1 valu, 2 mix
+template <int MODE>  // 0 salu, 1 valu, 2 mix 1:1, 3 mix 3 VALU : 1 SALU, 4 mix 6 VALU : 1 SALU
 __global__ __launch_bounds__(64) void probe(unsigned* out, unsigned seed) {
     unsigned s0 = seed, s1 = seed + 1, s2 = seed + 2, s3 = seed + 3;
     float v0 = (float)threadIdx.x, v1 = v0 + 1.0f, v2 = v0 + 2.0f, v3 = v0 + 3.0f;
@@ -43,12 +43,14 @@ __global__ __launch_bounds__(64) void probe(unsigned* out, unsigned seed) {
                 : "scc");
         }
         if constexpr (MODE != 0) {
-            asm volatile(
-                "v_add_f32 %0, 1.0, %0\n\t"
-                "v_add_f32 %1, 1.0, %1\n\t"
-                "v_add_f32 %2, 1.0, %2\n\t"
-                "v_add_f32 %3, 1.0, %3\n\t"
-                : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));
+#pragma unroll
+            for (int r = 0; r < (MODE == 3 ? 3 : MODE == 4 ? 6 : 1); ++r)
+                asm volatile(
+                    "v_add_f32 %0, 1.0, %0\n\t"
+                    "v_add_f32 %1, 1.0, %1\n\t"
+                    "v_add_f32 %2, 1.0, %2\n\t"
+                    "v_add_f32 %3, 1.0, %3\n\t"
+                    : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));
         }
     }
     const unsigned r = s0 ^ s1 ^ s2 ^ s3 ^ __float_as_uint(v0 + v1 + v2 + v3);
@@ -69,7 +71,7 @@ static int run(const char* name, int waves, unsigned* d) {
     float ms = 0;
     CHECK(hipEventElapsedTime(&ms, a, b));
     ms /= 5;
-    const double per_wave = (MODE == 2 ? 8.0 : 4.0) * ITERS;  // instructions per wave
+    const double per_wave = (MODE == 2 ? 8.0 : MODE == 3 ? 16.0 : MODE == 4 ? 28.0 : 4.0) * ITERS;  // instructions per wave
     const double cu_cycles = ms * 1e-3 * 2.4e9;                 // at 2.4 GHz
     std::printf("%-5s waves %7d  %.3f ms  %.3f wave-instructions per CU-cycle  (%.2f per SIMD-cycle)\n", name,
                 waves, ms, waves / 256.0 * per_wave / cu_cycles, waves / 1024.0 * per_wave / cu_cycles);
@@ -80,7 +82,9 @@ int main() {
     unsigned* d = nullptr;
     const int waves = 256 * 32 * 8;  // 8 rounds of 32 one-wave workgroups per CU
     CHECK(hipMalloc(&d, (size_t)waves * 64 * sizeof(unsigned)));
-    if (run<0>("salu", waves, d) || run<1>("valu", waves, d) || run<2>("mix", waves, d)) return 1;
+    if (run<0>("salu", waves, d) || run<1>("valu", waves, d) || run<2>("mix", waves, d) || run<3>("mix31", waves, d) ||
+        run<4>("mix61", waves, d))
+        return 1;
     CHECK(hipFree(d));
     return 0;
 }
