@@ -68,7 +68,7 @@ def parse(argv=None):
                     help="N>1: gather each frame before tracing the next (no double buffering)")
     ap.add_argument("--batch", type=int, default=0,
                     help="N>1: frames per RCCL gather (pipelined; 1 = one gather per frame).  0 = auto: 64, "
-                         "fewer for short runs (steps // 4, at least 8).  A batch boundary costs the host "
+                         "or the whole run when it is <= 128 frames (one batch).  A batch boundary costs the host "
                          "~100-200 us (codec calls, two collectives, a size read-back): at 16 frames per "
                          "gather that, not the GPU, bounded a rank's 1/8 share of 1080p (8.9 vs 3.0 us per "
                          "frame, tools/overhead_probe.sh)")
@@ -78,6 +78,10 @@ def parse(argv=None):
     ap.add_argument("--rank0-codec", action="store_true",
                     help="N>1 tiles: rank 0 encodes and decodes its own bands too (instead of rendering them "
                          "straight into its frames); the one-process rehearsal uses it to exercise the codec")
+    ap.add_argument("--no-speculate", action="store_true",
+                    help="N>1 tiles: read every batch's reduced wire size back before its gather (default: after "
+                         "the warm-up, gather at 1.25 x the largest wire per frame seen so far right behind the size "
+                         "reduce, check the reduced size before decoding and gather again when it was exceeded)")
     ap.add_argument("--compositor", choices=["auto", "on", "off"], default="auto",
                     help="N>1 tiles: rank 0 traces nothing and assembles the frames that ranks 1..N-1 "
                          "trace as a band world of N-1 (auto: N >= 8, where rank 0's own share plus the "
@@ -306,7 +310,11 @@ def main():
             sys.exit(2)
         sys.exit(subprocess.call(launch_command(sys.argv[1:], args.gpus, args.master_port)))
     if args.batch <= 0:
-        args.batch = 64 if args.steps >= 256 else max(8, args.steps // 4)
+        # N > 1: a short run is one batch (one size reduce + one gather + one decode: the fixed
+        # latency of each collective and of the host's size read-back dominates a handful of
+        # 1080p frames, and a pipeline of small batches pays it per batch); long runs pipeline
+        # batches of 64 frames
+        args.batch = args.steps if args.steps <= 128 else 64
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -488,12 +496,34 @@ def main():
 
     if launch_frames > 1:
         ctx.set_timing(4)  # launches of many frames: an event pair per 4 launches costs nothing
+    if tg is not None and not tg.idle and not tg.direct:
+        # size the codec's scratch for a whole batch before anything is timed (rt_encode_bands grows
+        # it on demand, behind a device synchronisation)
+        t_encode(tg.raw[0], tg.F, tg.wire[0], tg.size[0], stream)
+        torch.cuda.synchronize()
+    # warm-up: --warmup frames, then whole batches until every rank has run for --min-warmup-ms
+    # (the clock ramp); the ranks agree on each extra batch through an all_reduce, so every rank
+    # issues the same collectives
     run(args.warmup)
     finish()
     torch.cuda.synchronize()
+    warmup_done = args.warmup
+    t_w = time.perf_counter()
+    while True:
+        more = torch.tensor([1.0 if (time.perf_counter() - t_w) * 1e3 < args.min_warmup_ms else 0.0],
+                            dtype=torch.float64, device="cuda")
+        dist.all_reduce(more, op=dist.ReduceOp.MAX)
+        if float(more) == 0.0:
+            break
+        run(launch_frames)
+        finish()
+        torch.cuda.synchronize()
+        warmup_done += launch_frames
     ctx.reset_stats()
     if tg is not None:
         tg.bytes_sent = 0
+        if not args.no_speculate:
+            tg.set_capacity()  # the warm-up's largest wire per frame x 1.25 (checked per batch)
 
     if distributed:
         dist.barrier()
@@ -510,9 +540,9 @@ def main():
         stream.wait_stream(st_)
     ev1.record(stream)
     torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0  # this rank's time; the line reports the max over ranks
     if distributed:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
 
     st = ctx.stats()
     rays = st["primary_rays"] + st["reflect_rays"] + st["shadow_rays"]
@@ -550,6 +580,7 @@ def main():
             "n_gpus": world,
             "steps": steps,
             "warmup": args.warmup,
+            "warmup_effective": warmup_done,
             "ms_per_step": elapsed * 1e3 / steps,
             "fps": steps / elapsed,
             "higher_is_better": True,
@@ -612,6 +643,8 @@ def main():
             # wire bytes each rank shipped per frame (max over ranks, as gathered), vs the raw band set
             out["config"]["gather_wire_bytes_per_frame"] = tg.bytes_sent / steps
             out["config"]["gather_rgb24_bytes_per_frame"] = 3 * rb.slot_elems
+            out["config"]["gather_speculative"] = tg.capacity_per_frame is not None
+            out["config"]["gather_redone_batches"] = tg.redone
         if args.verify:
             out["verified_frames"] = verify_rings(ctx, tg, W, H, args.steps, torch)
         print(json.dumps(out), flush=True)

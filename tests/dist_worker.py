@@ -157,7 +157,7 @@ def run_batched(rank, world, port, cfg, width, height, band_rows, frames, per_ba
 
 
 def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batch, result_path, rank0_codec=False,
-              compositor=False):
+              compositor=False, speculate=0):
     """bench.py's default N>1 step: F frames per batch, tile-encoded band sets (host mirror of
     rt_encode_bands), size all_reduce + gather, rank 0 decodes every frame (host mirror of
     rt_decode_gathered) and checks it against the oracle."""
@@ -214,6 +214,8 @@ def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batc
                 ring.fill_(-7)
         for k in range(frames):
             if k % g.F == 0:
+                if speculate and k == 2 * g.F:  # the sizes of the first batches are known by now
+                    g.set_capacity(speculate)
                 g.begin_batch()
             if g.idle:  # the compositor rank renders nothing
                 g.commit()
@@ -231,6 +233,8 @@ def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batc
                     dst[l0 * width:(l0 + n) * width] = rows.reshape(-1)
             g.commit()
         g.drain()
+        if speculate and speculate < 1:
+            assert g.redone > 0, "a margin below 1 must force a gather at the real size"
         if rank == 0:
             bad = [k for k in range(frames)
                    if k not in got or not np.array_equal(got[k], pyoracle.render(scene_for(k), pyoracle.MODE_NEAREST, 2)[0])]

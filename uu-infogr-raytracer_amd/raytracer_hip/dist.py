@@ -314,6 +314,50 @@ class TileBandGather:
         self.decoded_ev = {}   # batch -> event after its decode (receive buffer / frame ring reusable)
         self.decoded = 0       # batches decoded (rank 0)
         self.bytes_sent = 0    # wire bytes gathered per rank (sum over batches)
+        self.max_per_frame = 0.0  # largest reduced wire size / frames of a batch seen so far
+        self.capacity_per_frame = None  # speculative gather size (set_capacity); None = wait for the size
+        self.redone = 0        # batches whose wire outgrew the speculative size (gathered again)
+
+    def set_capacity(self, margin=1.25):
+        """From now on gather each batch with a speculative size -- `margin` x the largest wire per
+        frame seen so far (every rank holds the same all-reduced sizes, so they agree without
+        communicating) -- issued right after the size reduce instead of after the host has read
+        the reduced size back.  The reduced size is still checked before the batch is decoded: a
+        batch whose largest wire exceeded the speculative size is gathered again at its real size
+        (every rank takes the same decision from the same reduced value)."""
+        if self.max_per_frame > 0:
+            self.capacity_per_frame = self.max_per_frame * margin
+
+    def _read_size(self, i, work):
+        import torch
+        if self.cuda:
+            with torch.cuda.stream(self.comm):
+                work.wait()
+                self.size_host[i:i + 1].copy_(self.size[i], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(self.comm)
+            ev.synchronize()
+        else:
+            work.wait()
+            self.size_host[i] = self.size[i][0]
+        return (int(self.size_host[i]) + 7) // 8 * 8
+
+    def _gather(self, b, i, n):
+        import torch
+        import torch.distributed as dist
+        j = b % 2
+        glist = None
+        if self.root:
+            slot = [(r - 1) % self.pworld if self.compositor else r for r in range(self.pworld)]
+            glist = [self.recv[j][q * self.rank_stride:q * self.rank_stride + n] for q in slot]
+        if self.cuda:
+            with torch.cuda.stream(self.comm):
+                if b - 2 in self.decoded_ev:  # receive buffer j was last read by decode b-2
+                    self.comm.wait_event(self.decoded_ev[b - 2])
+                for old in [x for x in self.decoded_ev if x < b - 4]:
+                    del self.decoded_ev[old]
+                return dist.gather(self.wire[i][:n], glist, dst=0, async_op=True)
+        return dist.gather(self.wire[i][:n], glist, dst=0, async_op=True)
 
     def ring_of(self, batch):
         return self.frames[batch % 3]
@@ -365,45 +409,33 @@ class TileBandGather:
         self.stage_b.append((b, n_frames, work))
         self.batch += 1
     def _stage_b(self):
-        import torch
-        import torch.distributed as dist
         b = self.stage_b[0][0]
         while self.stage_c and self.stage_c[0][0] <= b - 2:  # receive buffer b % 2 is free again
             self._stage_c()
         b, n_frames, work = self.stage_b.pop(0)
         i = b % 3
-        if self.cuda:
-            with torch.cuda.stream(self.comm):
-                work.wait()
-                self.size_host[i:i + 1].copy_(self.size[i], non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record(self.comm)
-            ev.synchronize()
-        else:
-            work.wait()
-            self.size_host[i] = self.size[i][0]
-        n = int(self.size_host[i])
-        n = (n + 7) // 8 * 8
+        if self.capacity_per_frame is not None:
+            # speculative size: gather now, check the reduced size in stage C
+            n = min(self.rank_stride, (int(self.capacity_per_frame * n_frames) + 7) // 8 * 8)
+            self.stage_c.append((b, n_frames, self._gather(b, i, n), (work, n)))
+            return
+        n = self._read_size(i, work)
+        self.max_per_frame = max(self.max_per_frame, n / n_frames)
         self.bytes_sent += n
-        j = b % 2
-        glist = None
-        if self.root:
-            slot = [(r - 1) % self.pworld if self.compositor else r for r in range(self.pworld)]
-            glist = [self.recv[j][q * self.rank_stride:q * self.rank_stride + n] for q in slot]
-        if self.cuda:
-            with torch.cuda.stream(self.comm):
-                if b - 2 in self.decoded_ev:  # receive buffer j was last read by decode b-2
-                    self.comm.wait_event(self.decoded_ev[b - 2])
-                for old in [x for x in self.decoded_ev if x < b - 4]:
-                    del self.decoded_ev[old]
-                gw = dist.gather(self.wire[i][:n], glist, dst=0, async_op=True)
-        else:
-            gw = dist.gather(self.wire[i][:n], glist, dst=0, async_op=True)
-        self.stage_c.append((b, n_frames, gw))
+        self.stage_c.append((b, n_frames, self._gather(b, i, n), None))
 
     def _stage_c(self):
         import torch
-        b, n_frames, gw = self.stage_c.pop(0)
+        b, n_frames, gw, spec = self.stage_c.pop(0)
+        if spec is not None:  # speculative gather: the reduced size decides whether it sufficed
+            work, n_spec = spec
+            n = self._read_size(b % 3, work)  # (reduced before the gather was issued)
+            self.max_per_frame = max(self.max_per_frame, n / n_frames)
+            self.bytes_sent += n_spec
+            if n > n_spec:  # some wire outgrew it (every rank sees the same n): gather again, in full
+                self.redone += 1  # (collectives of one group run in issue order)
+                gw = self._gather(b, b % 3, n)
+                self.bytes_sent += n
         if self.cuda:
             with torch.cuda.stream(self.dec):
                 gw.wait()
