@@ -101,7 +101,8 @@ struct Device {
 
 struct SceneLayout {
     int S = 0, P = 0, L = 0, limit = 0;
-    size_t off_sph = 0, off_mat = 0, off_pl = 0, off_li = 0, off_cull = 0, bytes = 0;
+    size_t off_sph = 0, off_mat = 0, off_pl = 0, off_li = 0, off_cull = 0, off_shcull = 0, bytes = 0;
+    bool has_shcull = false;
     bool generic_pow = false;        // a specular material with n not in {0.5, 1, 2}
     std::vector<DevSphere> host_sph;  // for the per-frame primary constants
 };
@@ -352,6 +353,7 @@ void scene_params(const rt_ctx* ctx, const Device& d, LaunchParams& lp) {
     lp.pl = (const DevPlane*)(base + L.off_pl);
     lp.li = (const DevLight*)(base + L.off_li);
     lp.scull = (const DevSphereCull*)(base + L.off_cull);
+    lp.shcull = L.has_shcull ? (const DevShadowCull*)(base + L.off_shcull) : nullptr;
     lp.S = L.S, lp.P = L.P, lp.L = L.L, lp.limit = L.limit;
     lp.counters = d.d_counters;
 }
@@ -559,7 +561,9 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
     L.off_pl = al(L.off_mat + sizeof(DevMaterial) * (size_t)(n_spheres + n_planes));
     L.off_li = al(L.off_pl + sizeof(DevPlane) * (size_t)n_planes);
     L.off_cull = al(L.off_li + sizeof(DevLight) * (size_t)n_lights);
-    L.bytes = al(L.off_cull + sizeof(DevSphereCull) * (size_t)n_spheres) + 256;
+    L.off_shcull = al(L.off_cull + sizeof(DevSphereCull) * (size_t)n_spheres);
+    L.has_shcull = (long long)n_lights * (long long)n_spheres <= SHADOW_CULL_MAX_ENTRIES;
+    L.bytes = al(L.off_shcull + (L.has_shcull ? sizeof(DevShadowCull) * (size_t)n_lights * (size_t)n_spheres : 0)) + 256;
 
     std::vector<unsigned char> blob(L.bytes, 0);
     DevSphere* sph = (DevSphere*)(blob.data() + L.off_sph);
@@ -616,6 +620,21 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
         d.ux = (float)U[0], d.uy = (float)U[1], d.uz = (float)U[2];
         d.vx = (float)V[0], d.vy = (float)V[1], d.vz = (float)V[2];
         li[i] = d;
+    }
+    if (L.has_shcull) {  // sphere centres in each light's shadow-cull frame (culling only)
+        DevShadowCull* sc = (DevShadowCull*)(blob.data() + L.off_shcull);
+        for (int j = 0; j < n_lights; ++j)
+            for (int i = 0; i < n_spheres; ++i) {
+                const DevLight& d = li[j];
+                const double c[3] = {cull[i].cx, cull[i].cy, cull[i].cz};
+                const double clen = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+                DevShadowCull& e = sc[(size_t)j * (size_t)n_spheres + (size_t)i];
+                e.cu = (float)(c[0] * d.ux + c[1] * d.uy + c[2] * d.uz);
+                e.cv = (float)(c[0] * d.vx + c[1] * d.vy + c[2] * d.vz);
+                e.ca = (float)(c[0] * d.ax + c[1] * d.ay + c[2] * d.az);
+                // r' + 2^-18 |C|, rounded up (NaN / inf stay: the kernel keeps such spheres)
+                e.rr = std::nextafter((float)((double)cull[i].rr + 0x1p-18 * clen), INFINITY);
+            }
     }
     for (int i = 0; i < n_spheres + n_planes; ++i)
         if ((mat[i].flags & MAT_SPEC) && mat[i].pow_kind == POW_GENERIC) L.generic_pow = true;

@@ -63,6 +63,14 @@ struct DevSphereCull {
     float cx, cy, cz, rr;
 };
 
+// Per-(light, sphere) shadow-cull record (culling only): the sphere centre in the light's frame
+// (C.U, C.V, C.A, rounded from double) and r' + 2^-18 |C| (the projection-error allowance,
+// rt_kernel.hip shadow_cull_mask).  [L][S], built when L * S <= SHADOW_CULL_MAX_ENTRIES.
+struct DevShadowCull {
+    float cu, cv, ca, rr;
+};
+constexpr long long SHADOW_CULL_MAX_ENTRIES = 1LL << 16;
+
 // Work counters: each workgroup adds its totals into slot (block id % COUNTER_SLOTS) so that
 // the atomics of thousands of workgroups do not serialise on one address.  Per slot:
 // reflected segments and shadow rays of the visible path (every launch), and the executed
@@ -100,6 +108,7 @@ struct LaunchParams {
     const DevPlane* pl;
     const DevLight* li;
     const DevSphereCull* scull;  // [S]
+    const DevShadowCull* shcull;  // [L][S] or NULL (the kernel projects the centres itself)
     const float* lxt;  // [W]: ((float)x / W - 0.5f) * pw, TracePixel :963-965
     const float* lyt;  // [H]: ((float)y / H - 0.5f) * ph
     int S, P, L, limit;

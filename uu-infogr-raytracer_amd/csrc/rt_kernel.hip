@@ -844,66 +844,77 @@ __device__ __forceinline__ unsigned long long cull_mask(const LaunchParams& p, c
 
 // Shadow bundles.  Every shadow ray of light l has the same direction p_l (the light
 // POSITION, Q2), so a sphere can block lane k only if the line {hp_k + s p_l} passes within
-// r of its centre: a 2-D test in the light's frame (U, V, A ~ p_l/|p_l|, host-built), where
-// the wave's hit points spread by R_perp across A and by [-R_neg, R_pos] along it.  Cull
-// rules (same error analysis and 2^-8 margin as cull_mask, with |u| bounded by the L1 norm
-// of the frame coordinates plus the spreads): line miss if |w_perp| - R_perp > r' + mgn;
-// behind (b >= 0 for every lane) if -w_A - R_neg > mgn, where w = C - O.
-struct ShadowBundle {
+// r of its centre: a 2-D test in the light's frame (U, V, A ~ p_l/|p_l|, host-built).  One bound
+// serves every light of a shaded level: the ball (O, R) around the first diffuse lane's hit
+// point that holds every diffuse lane's hit point, so the hit points spread by at most R across
+// and along any light's axis.  Cull rules (same error analysis and 2^-8 margin as cull_mask,
+// |C - O| bounded by the L1 norm of the frame coordinates): line miss if |w_perp| - R > r' + mgn;
+// behind (b >= 0 for every lane) if -w_A - R > mgn, where w = C - O.  Per light the work is the
+// projection of O (uniform) and the cull itself, with the sphere centres already in each light's
+// frame (DevShadowCull, host-built in double; the rounding of those projections and of O's is
+// covered by the 2^-18 (|C| + |O|) allowance, far above their 2^-22 (|C| + |O|) error).  Against
+// a bound per light from its exact perpendicular / axial spreads (three wave reductions per
+// light): C4 -2.6 %, C5 -7.5 % (profiles/ab/r02_shadow_sphere.txt).
+struct ShadowSphere {
     f3 O;
-    float Rp, Rneg, Rsum;  // perpendicular spread, backward spread, Rp + Rneg + Rpos
+    float R, omgn;  // radius (rounded up) and 2^-18 |O|
     bool ok;
 };
 
-__device__ __forceinline__ ShadowBundle make_shadow_bundle(f3 hp, const DevLight& l, bool active) {
-    ShadowBundle B;
+__device__ __forceinline__ ShadowSphere make_shadow_sphere(f3 hp, bool active) {
+    ShadowSphere S;
     const unsigned long long m = __builtin_amdgcn_ballot_w64(active);
-    B.ok = false;
-    B.Rp = B.Rneg = B.Rsum = 0.0f;
-    B.O = hp;
-    if (m == 0) return B;
-    B.O = readlane3(hp, __builtin_ctzll(m));
-    float perp2 = 0.0f, neg = 0.0f, pos = 0.0f;
+    S.ok = false;
+    S.R = 0.0f;
+    S.omgn = 0.0f;
+    S.O = hp;
+    if (m == 0) return S;
+    S.O = readlane3(hp, __builtin_ctzll(m));
+    float e = 0.0f;
     bool bad = false;
     if (active) {
-        const f3 e = sub(hp, B.O);
-        const float eu = dot(e, mk(l.ux, l.uy, l.uz));
-        const float ev = dot(e, mk(l.vx, l.vy, l.vz));
-        const float ea = dot(e, mk(l.ax, l.ay, l.az));
-        perp2 = eu * eu + ev * ev;
-        neg = nmax0(-ea);
-        pos = nmax0(ea);
-        bad = !(perp2 < 0x1p80f) || !(neg < 0x1p40f) || !(pos < 0x1p40f);  // also NaN / inf
+        e = clen3(sub(hp, S.O));
+        bad = !(e < 0x1p40f);  // also NaN / inf
     }
     bad = __builtin_amdgcn_ballot_w64(bad) != 0;
-    const float Rp2 = wave_max(perp2);
-    B.Rp = __builtin_sqrtf(Rp2) * (1.0f + 0x1p-10f) + 0x1p-60f;
-    B.Rneg = wave_max(neg) * (1.0f + 0x1p-10f) + 0x1p-60f;
-    const float Rpos = wave_max(pos) * (1.0f + 0x1p-10f) + 0x1p-60f;
-    B.Rsum = B.Rp + B.Rneg + Rpos;
-    B.ok = !bad && l.a >= 0x1p-40f && l.a <= 0x1p40f && l.a2 < __builtin_inff() && B.Rsum < 0x1p41f;
-    return B;
+    S.R = wave_max(e) * (1.0f + 0x1p-10f) + 0x1p-60f;
+    const float olen = clen3(S.O);
+    S.omgn = 0x1p-18f * olen * (1.0f + 0x1p-10f);
+    S.ok = !bad && S.R < 0x1p38f && olen < 0x1p40f;
+    return S;
 }
 
-// Candidate mask of spheres [base, base+n) (n <= 64) for shadow bundle B.  Converged call.
-__device__ __forceinline__ unsigned long long shadow_cull_mask(const LaunchParams& p, const ShadowBundle& B,
-                                                               const DevLight& l, int base, int n) {
+// Candidate mask of spheres [base, base+n) (n <= 64) for the shadow rays of light li from the
+// ball S.  Converged call.
+__device__ __forceinline__ unsigned long long shadow_sphere_cull(const LaunchParams& p, const ShadowSphere& S,
+                                                                 const DevLight& l, int li, int base, int n) {
     const int lane = threadIdx.x & 63;
+    const bool ok = S.ok && l.a >= 0x1p-40f && l.a <= 0x1p40f && l.a2 < __builtin_inff();  // uniform
+    // O in the light's frame (uniform)
+    const float ou = dot(S.O, mk(l.ux, l.uy, l.uz)), ov = dot(S.O, mk(l.vx, l.vy, l.vz));
+    const float oa = dot(S.O, mk(l.ax, l.ay, l.az));
     bool cand = false;
     if (lane < n) {
         cand = true;
-        if (B.ok) {
-            const DevSphereCull s = p.scull[base + lane];
-            const f3 w = sub(mk(s.cx, s.cy, s.cz), B.O);
-            const float wu = dot(w, mk(l.ux, l.uy, l.uz));
-            const float wv = dot(w, mk(l.vx, l.vy, l.vz));
-            const float wa = dot(w, mk(l.ax, l.ay, l.az));
-            const float dc = __builtin_fabsf(wu) + __builtin_fabsf(wv) + __builtin_fabsf(wa);  // >= |w|
-            if (s.rr >= 0x1p-50f && dc >= 0x1p-30f && dc < 0x1p40f) {
-                const float mgn = 0x1p-8f * (dc + B.Rsum);
-                const float T = B.Rp + s.rr + mgn;
+        if (ok) {
+            DevShadowCull c;
+            if (p.shcull) {
+                c = p.shcull[(size_t)li * (size_t)p.S + (size_t)(base + lane)];
+            } else {  // (scenes with too many light-sphere pairs for the table)
+                const DevSphereCull q = p.scull[base + lane];
+                const f3 C = mk(q.cx, q.cy, q.cz);
+                c.cu = dot(C, mk(l.ux, l.uy, l.uz));
+                c.cv = dot(C, mk(l.vx, l.vy, l.vz));
+                c.ca = dot(C, mk(l.ax, l.ay, l.az));
+                c.rr = q.rr + 0x1p-18f * clen3(C) * (1.0f + 0x1p-10f);
+            }
+            const float wu = c.cu - ou, wv = c.cv - ov, wa = c.ca - oa;
+            const float dc = __builtin_fabsf(wu) + __builtin_fabsf(wv) + __builtin_fabsf(wa);  // >= |C - O|
+            if (c.rr >= 0x1p-50f && dc >= 0x1p-30f && dc < 0x1p40f) {
+                const float mgn = 0x1p-8f * (dc + 3.0f * S.R) + S.omgn;
+                const float T = S.R + c.rr + mgn;
                 const bool line = wu * wu + wv * wv > T * T;
-                const bool behind = -wa - B.Rneg > mgn;
+                const bool behind = -wa - S.R > mgn;
                 cand = !(line || behind);  // NaN anywhere -> candidate
             }
         }
@@ -1025,6 +1036,7 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
         // sphere: (1 / t) * t (:866);  plane: (float)(1 / Math.Pow(t, 2)) (:754), exact as 1/(t*t) in f64
         const float att = is_sphere ? cr_rcp(t) * t : (float)(1.0 / ((double)t * (double)t));
         const f3 kd = mk(m.kd[0], m.kd[1], m.kd[2]);
+        const ShadowSphere SS = make_shadow_sphere(hp, diff);  // one bound for every light's shadow rays
         for (int li = 0; li < p.L; ++li) {
             const DevLight& l = p.li[li];
             const f3 lp = mk(l.px, l.py, l.pz);
@@ -1043,11 +1055,10 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
             bool blocked = !need;
             if (__builtin_amdgcn_ballot_w64(need) != 0) {  // some lane's pixel depends on this test
                 tl.shadow(need);
-                const ShadowBundle B = make_shadow_bundle(hp, l, need);
-                const f3 hs = need ? hp : B.O;  // idle lanes mirror a shading lane (results ignored)
+                const f3 hs = need ? hp : SS.O;  // idle lanes mirror a shading lane (results ignored)
                 for (int base = 0; base < p.S; base += 64) {
                     const int n = min(64, p.S - base);
-                    unsigned long long mk64 = shadow_cull_mask(p, B, l, base, n);
+                    unsigned long long mk64 = shadow_sphere_cull(p, SS, l, li, base, n);
                     // candidates two at a time: independent tests (ILP across the sqrt chains),
                     // one pair of sphere loads and one exit ballot per pair; an odd last
                     // candidate is tested twice (the OR is unchanged)
@@ -1199,14 +1210,28 @@ __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int
     return cnt;
 }
 
+// Occupancy: a wave's SGPRs count against a per-SIMD file of ~800 (waves per SIMD <=
+// 800 / (ceil(sgpr / 16) * 16 + 16), MI355X_MICROARCH.md 'Residency'): the compiler's 93-106
+// SGPRs admitted 6-7 waves per SIMD whatever its report said.  Capped at 80 (a few uniform values
+// spilled to VGPR lanes) and 64 VGPRs (8 waves): C4 -2.6 %, C5 -7.5 %.  Not with GPOW (the f64
+// Math.Pow path would spill ~150 B/lane to scratch).  The direct kernel needs no cap (79 SGPRs, 48
+// VGPRs).
 template <int K, bool GPOW, bool STATS>
-__global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel(LaunchParams p) {
+__device__ __forceinline__ void bundle_kernel_body(const LaunchParams& p) {
     constexpr int LDS_LEVELS = StackFor<K>::lds_levels;  // LdsStack slots, else unused
     __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
     __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * WG_THREADS : 1];
     Tally<STATS> tl;
     const unsigned cnt = trace_tile_bundle<K, GPOW>(p, blockIdx.x, stk_lv, stk_dv, tl);
     add_counters<STATS>(p, threadIdx.x & 63, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
+}
+template <int K, bool STATS>
+__global__ __launch_bounds__(WG_THREADS, 8) __attribute__((amdgpu_num_sgpr(80))) void trace_bundle_kernel(LaunchParams p) {
+    bundle_kernel_body<K, false, STATS>(p);
+}
+template <int K, bool STATS>
+__global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel_gpow(LaunchParams p) {
+    bundle_kernel_body<K, true, STATS>(p);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1331,7 +1356,7 @@ template <bool GPOW, bool STATS>
 struct BundleK {
     template <int K>
     struct at {
-        static constexpr auto fn = trace_bundle_kernel<K, GPOW, STATS>;
+        static constexpr auto fn = GPOW ? trace_bundle_kernel_gpow<K, STATS> : trace_bundle_kernel<K, STATS>;
     };
 };
 
