@@ -796,7 +796,10 @@ __device__ __forceinline__ Bundle make_bundle(f3 o, f3 d, bool active, bool dir_
         return B;
     }
     const int ref = __builtin_ctzll(m);
-    B.O = readlane3(o, ref);
+    {  // midway between the first and the last active lane's origins (see make_shadow_sphere)
+        const f3 a = readlane3(o, ref), b = readlane3(o, 63 - __builtin_clzll(m));
+        B.O = scale(add(a, b), 0.5f);
+    }
     const f3 dref = readlane3(d, ref);
     B.A = cnormalize(dref);
     float e = 0.0f, f = 0.0f;
@@ -869,7 +872,13 @@ __device__ __forceinline__ ShadowSphere make_shadow_sphere(f3 hp, bool active) {
     S.omgn = 0.0f;
     S.O = hp;
     if (m == 0) return S;
-    S.O = readlane3(hp, __builtin_ctzll(m));
+    {
+        // centre: midway between the first and the last active lane's hit points (lanes 0 and 63
+        // are opposite corners of the 8x8 tile), which roughly halves R against either of them
+        // (C4 -4.3 %, C5 -3.8 %, profiles/ab/r02_bundle_centre.txt); R is measured from it
+        const f3 a = readlane3(hp, __builtin_ctzll(m)), b = readlane3(hp, 63 - __builtin_clzll(m));
+        S.O = scale(add(a, b), 0.5f);
+    }
     float e = 0.0f;
     bool bad = false;
     if (active) {
