@@ -34,7 +34,8 @@ internal static class Native {
     [DllImport(Lib)] internal static extern int rt_unregister_host(IntPtr ctx, IntPtr p);
     [DllImport(Lib)] internal static extern int rt_render(IntPtr ctx, int w, int h, IntPtr pixels);
     // ABI v2+ additions (not needed by the synchronous Tick below): pipelined frames, debug view, timing
-    // (ABI 4's multi-process pieces -- batched band launches, tile codec -- are declared in INTEGRATION.md)
+    // (ABI 4/5's multi-process and diagnostic pieces -- batched band launches, tile codec, rt_create_ex,
+    // rt_count_work -- are declared in INTEGRATION.md)
     [StructLayout(LayoutKind.Sequential)] internal struct Segment { public Vec3 Origin, End; public int Kind, Pixel; }
     [DllImport(Lib)] internal static extern int rt_render_async(IntPtr ctx, int w, int h, IntPtr pixels);
     [DllImport(Lib)] internal static extern int rt_wait(IntPtr ctx);
