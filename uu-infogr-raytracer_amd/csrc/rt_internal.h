@@ -65,7 +65,8 @@ struct DevSphereCull {
 
 // Per-(light, sphere) shadow-cull record (culling only): the sphere centre in the light's frame
 // (C.U, C.V, C.A, rounded from double) and r' + 2^-18 |C| (the projection-error allowance,
-// rt_kernel.hip shadow_cull_mask).  [L][S], built when L * S <= SHADOW_CULL_MAX_ENTRIES.
+// rt_kernel.hip shadow_sphere_cull).  [L][S], built when L * S <= SHADOW_CULL_MAX_ENTRIES (larger
+// scenes trace their shadow rays without culling).
 struct DevShadowCull {
     float cu, cv, ca, rr;
 };
@@ -108,7 +109,7 @@ struct LaunchParams {
     const DevPlane* pl;
     const DevLight* li;
     const DevSphereCull* scull;  // [S]
-    const DevShadowCull* shcull;  // [L][S] or NULL (the kernel projects the centres itself)
+    const DevShadowCull* shcull;  // [L][S] or NULL (no shadow culling)
     const float* lxt;  // [W]: ((float)x / W - 0.5f) * pw, TracePixel :963-965
     const float* lyt;  // [H]: ((float)y / H - 0.5f) * ph
     int S, P, L, limit;

@@ -824,25 +824,21 @@ __device__ __forceinline__ Bundle make_bundle(f3 o, f3 d, bool active, bool dir_
 
 // Candidate mask of spheres [base, base+n) (n <= 64) for bundle B.  Converged call.
 __device__ __forceinline__ unsigned long long cull_mask(const LaunchParams& p, const Bundle& B, int base, int n) {
+    // branch-free (no exec-mask bookkeeping on the scalar unit): every lane loads and tests, lanes
+    // >= n are dropped from the ballot; a sphere is culled only when the bundle allows culling,
+    // its record is in range and one of the rules holds (NaN anywhere -> candidate)
     const int lane = threadIdx.x & 63;
-    bool cand = false;
-    if (lane < n) {
-        cand = true;
-        if (B.ok) {
-            const DevSphereCull s = p.scull[base + lane];
-            const f3 w = sub(mk(s.cx, s.cy, s.cz), B.O);
-            const float dc = clen3(w) * (1.0f + 0x1p-20f);
-            if (s.rr >= 0x1p-50f && dc >= 0x1p-30f && dc < 0x1p40f) {
-                const float rr = s.rr;
-                const float mgn = 0x1p-8f * (dc + B.R);
-                const float x = clen3(cross3(w, B.A));
-                const bool line = (x - dc * B.delta - B.R) > rr + mgn;
-                const bool behind = (-dot(w, B.A) - dc * B.delta - B.R * (1.0f + B.delta)) > mgn;
-                cand = !(line || behind);  // NaN anywhere -> candidate
-            }
-        }
-    }
-    return __builtin_amdgcn_ballot_w64(cand);
+    const bool in = lane < n;
+    const DevSphereCull s = p.scull[base + (in ? lane : 0)];
+    const f3 w = sub(mk(s.cx, s.cy, s.cz), B.O);
+    const float dc = clen3(w) * (1.0f + 0x1p-20f);
+    const float mgn = 0x1p-8f * (dc + B.R);
+    const float x = clen3(cross3(w, B.A));
+    const bool line = (x - dc * B.delta - B.R) > s.rr + mgn;
+    const bool behind = (-dot(w, B.A) - dc * B.delta - B.R * (1.0f + B.delta)) > mgn;
+    const bool valid = s.rr >= 0x1p-50f && dc >= 0x1p-30f && dc < 0x1p40f;
+    const bool cull = B.ok && valid && (line || behind);
+    return __builtin_amdgcn_ballot_w64(in && !cull);
 }
 
 // Shadow bundles.  Every shadow ray of light l has the same direction p_l (the light
@@ -898,37 +894,21 @@ __device__ __forceinline__ ShadowSphere make_shadow_sphere(f3 hp, bool active) {
 __device__ __forceinline__ unsigned long long shadow_sphere_cull(const LaunchParams& p, const ShadowSphere& S,
                                                                  const DevLight& l, int li, int base, int n) {
     const int lane = threadIdx.x & 63;
-    const bool ok = S.ok && l.a >= 0x1p-40f && l.a <= 0x1p40f && l.a2 < __builtin_inff();  // uniform
-    // O in the light's frame (uniform)
+    const bool in = lane < n;
+    const bool ok = S.ok && p.shcull != nullptr && l.a >= 0x1p-40f && l.a <= 0x1p40f && l.a2 < __builtin_inff();
+    if (!ok) return __builtin_amdgcn_ballot_w64(in);  // (uniform) no culling: every sphere is a candidate
+    // O in the light's frame (uniform); branch-free per lane, as cull_mask
     const float ou = dot(S.O, mk(l.ux, l.uy, l.uz)), ov = dot(S.O, mk(l.vx, l.vy, l.vz));
     const float oa = dot(S.O, mk(l.ax, l.ay, l.az));
-    bool cand = false;
-    if (lane < n) {
-        cand = true;
-        if (ok) {
-            DevShadowCull c;
-            if (p.shcull) {
-                c = p.shcull[(size_t)li * (size_t)p.S + (size_t)(base + lane)];
-            } else {  // (scenes with too many light-sphere pairs for the table)
-                const DevSphereCull q = p.scull[base + lane];
-                const f3 C = mk(q.cx, q.cy, q.cz);
-                c.cu = dot(C, mk(l.ux, l.uy, l.uz));
-                c.cv = dot(C, mk(l.vx, l.vy, l.vz));
-                c.ca = dot(C, mk(l.ax, l.ay, l.az));
-                c.rr = q.rr + 0x1p-18f * clen3(C) * (1.0f + 0x1p-10f);
-            }
-            const float wu = c.cu - ou, wv = c.cv - ov, wa = c.ca - oa;
-            const float dc = __builtin_fabsf(wu) + __builtin_fabsf(wv) + __builtin_fabsf(wa);  // >= |C - O|
-            if (c.rr >= 0x1p-50f && dc >= 0x1p-30f && dc < 0x1p40f) {
-                const float mgn = 0x1p-8f * (dc + 3.0f * S.R) + S.omgn;
-                const float T = S.R + c.rr + mgn;
-                const bool line = wu * wu + wv * wv > T * T;
-                const bool behind = -wa - S.R > mgn;
-                cand = !(line || behind);  // NaN anywhere -> candidate
-            }
-        }
-    }
-    return __builtin_amdgcn_ballot_w64(cand);
+    const DevShadowCull c = p.shcull[(size_t)li * (size_t)p.S + (size_t)(base + (in ? lane : 0))];
+    const float wu = c.cu - ou, wv = c.cv - ov, wa = c.ca - oa;
+    const float dc = __builtin_fabsf(wu) + __builtin_fabsf(wv) + __builtin_fabsf(wa);  // >= |C - O|
+    const float mgn = 0x1p-8f * (dc + 3.0f * S.R) + S.omgn;
+    const float T = S.R + c.rr + mgn;
+    const bool line = wu * wu + wv * wv > T * T;
+    const bool behind = -wa - S.R > mgn;
+    const bool valid = c.rr >= 0x1p-50f && dc >= 0x1p-30f && dc < 0x1p40f;
+    return __builtin_amdgcn_ballot_w64(in && !(valid && (line || behind)));  // NaN anywhere -> candidate
 }
 
 // BUNDLE path.  Nearest hit of one segment for every active lane (converged call).  PRIMARY: TracePixel's
