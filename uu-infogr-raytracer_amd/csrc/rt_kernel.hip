@@ -911,6 +911,32 @@ __device__ __forceinline__ unsigned long long shadow_sphere_cull(const LaunchPar
     return __builtin_amdgcn_ballot_w64(in && !(valid && (line || behind)));  // NaN anywhere -> candidate
 }
 
+// Exact tests of the candidate spheres m (bits relative to `base`) of one bundle segment, in
+// ascending order (the reference's tie rules), for every lane (idle lanes trace a copy of an active
+// lane's ray).  A2OK: 2a finite-positive on every lane.
+template <bool PRIMARY, bool A2OK, typename T>
+__device__ __forceinline__ void bundle_candidates(const LaunchParams& p, unsigned long long m, int base, f3 o, f3 d,
+                                                  float a2, float a4, bool a2_ok, bool active, float& best_s,
+                                                  int& win_s, T& tl) {
+    while (m) {
+        const int i = base + (int)__builtin_ctzll(m);
+        m &= m - 1;
+        tl.sphere(active);
+        float t;
+        if (PRIMARY && p.prim_const) {
+            // o == camera: oc = cam - c and c = oc.oc - r^2 are per-frame constants (:614-619)
+            const PrimConst pc = p.pc[i];
+            const float b = 2.0f * dot(mk(pc.ocx, pc.ocy, pc.ocz), d);
+            const float disc = b * b - a4 * pc.c;
+            t = A2OK ? root_t1(b, disc, a2) : (a2_ok ? root_t1(b, disc, a2) : root_full(b, disc, a2));
+        } else {
+            t = sphere_t<A2OK>(o, d, a2, a4, a2_ok, p.sph[i]);
+        }
+        if (PRIMARY) take_primary(t, i, best_s, win_s);
+        else take_secondary(t, i, best_s, win_s);
+    }
+}
+
 // BUNDLE path.  Nearest hit of one segment for every active lane (converged call).  PRIMARY: TracePixel's
 // rule (:977, :987, :993) with the per-frame camera-relative constants; otherwise
 // TraceSecondaryRay's asymmetric rule (:804-806, :819-821, :825).
@@ -940,37 +966,12 @@ __device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d,
     for (int base = 0; base < p.S; base += 64) {
         const int n = min(64, p.S - base);
         unsigned long long m = use_box ? pmask : cull_mask(p, B, base, n);  // use_box: S <= 64
-        auto test = [&](int i) {
-            if (PRIMARY && p.prim_const) {
-                // o == camera: oc = cam - c and c = oc.oc - r^2 are per-frame constants (:614-619)
-                const PrimConst pc = p.pc[i];
-                const float b = 2.0f * dot(mk(pc.ocx, pc.ocy, pc.ocz), d);
-                const float disc = b * b - a4 * pc.c;
-                return a2_ok ? root_t1(b, disc, a2) : root_full(b, disc, a2);
-            }
-            return sphere_t<false>(o, d, a2, a4, a2_ok, p.sph[i]);
-        };
-        auto take = [&](float t, int i) {
-            if (PRIMARY) {
-                if (t > 0.0f && best_s > t) {
-                    best_s = t;
-                    win_s = i;
-                }
-            } else {
-                const float tm = t - 0.01f;
-                if (tm > 0.0f && tm < best_s) {
-                    best_s = t;
-                    win_s = i;
-                }
-            }
-        };
-        // (pairing the candidates as in the shadow loop measured +0.8 % on C4)
-        while (m) {
-            const int i = base + (int)__builtin_ctzll(m);
-            m &= m - 1;
-            tl.sphere(active);
-            take(test(i), i);
-        }
+        // candidates in ascending order, selection by selects (take_*, no per-lane branches); the
+        // root sequence is chosen once per wave (2a finite-positive on every lane: the usual case)
+        if (__builtin_amdgcn_ballot_w64(!a2_ok) == 0)
+            bundle_candidates<PRIMARY, true>(p, m, base, o, d, a2, a4, a2_ok, active, best_s, win_s, tl);
+        else
+            bundle_candidates<PRIMARY, false>(p, m, base, o, d, a2, a4, a2_ok, active, best_s, win_s, tl);
     }
     float best_p = __builtin_inff();
     int win_p = -1;
@@ -980,11 +981,7 @@ __device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d,
     } else {
         for (int i = 0; i < p.P; ++i) {
             tl.plane(active);
-            const float t = plane_t(o, d, p.pl[i]);
-            if (t > 0.0f && t < best_p) {
-                best_p = t;
-                win_p = i;
-            }
+            take_primary(plane_t(o, d, p.pl[i]), i, best_p, win_p);  // t > 0 && t < best
         }
     }
     if (!active) return Hit{0.0f, HIT_NONE};
@@ -1173,11 +1170,7 @@ __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int
             int win_p = -1;
             for (int i = 0; i < p.P; ++i) {
                 tl.plane(active);
-                const float t = plane_t(o, d, p.pl[i]);
-                if (t > 0.0f && t < best_p) {
-                    best_p = t;
-                    win_p = i;
-                }
+                take_primary(plane_t(o, d, p.pl[i]), i, best_p, win_p);  // t > 0 && t < best
             }
             const bool need = active && win_p >= 0 && best_p - 0.01f > 0.0f;
             h = Hit{0.0f, HIT_NONE};
