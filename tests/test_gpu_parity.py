@@ -84,6 +84,24 @@ def test_dense_random_scenes_vs_oracle(gpu_ctx, oracle, seed):
     assert ray_counts(st) == {k: ost[k] for k in ("primary_rays", "reflect_rays", "shadow_rays")}
 
 
+@pytest.mark.parametrize("n_lights", [3000, 4200])
+def test_many_lights_with_and_without_the_shadow_cull_table(gpu_ctx, oracle, n_lights):
+    """The bundle kernel's shadow culling reads the sphere centres pre-projected into each light's
+    frame from a [lights][spheres] table built when lights x spheres <= 65536 (16 spheres: 3000
+    lights have one, 4200 do not and trace their shadow rays unculled); both must match."""
+    import random_scenes
+    base = random_scenes.random_scene(101, 24, 16, dense=True)
+    rng = np.random.default_rng(n_lights)
+    lights = [scenes.Light(tuple(float(np.float32(x)) for x in rng.uniform(-30, 30, 3)),
+                           float(np.float32(rng.uniform(0.0002, 0.0004)))) for _ in range(n_lights)]
+    sc = scenes.Scene(f"lights{n_lights}", 24, 16, base.spheres[:16], base.planes, lights, base.ambient, 2,
+                      base.camera)
+    px, st = render_gpu(gpu_ctx, sc)
+    want, ost = oracle.render(sc, oracle.MODE_NEAREST, 8)
+    assert_same(px, want, sc.name)
+    assert ray_counts(st) == {k: ost[k] for k in ("primary_rays", "reflect_rays", "shadow_rays")}
+
+
 @pytest.mark.parametrize("seed", list(range(200)))
 def test_camera_sweep_vs_oracle(gpu_ctx, oracle, seed):
     """Primary screen boxes (and both kernels' primary paths) under arbitrary views."""
