@@ -7,8 +7,9 @@ on the configuration named by --config (default C2 = BASELINE.json configs[1]: 1
 to HBM.
 
 N = 1: the timed frames run as balanced launches of up to 64 frames (rt_render_bands_batch),
-one launch in flight, every launch timed alone with a HIP event pair (roofline.kernel_avg_ms,
-which rocprofv3's kernel trace of the same command reproduces).  C3 (the north-star config:
+one launch in flight, back to back on one stream: HIP events around the timed region / launches
+give roofline.kernel_avg_ms (which rocprofv3's kernel trace of the same command reproduces); an
+untimed second pass times each launch with its own event pair (kernel_avg_ms_launch_events).  C3 (the north-star config:
 depth 4, 2 lights) is measured in the same run ("also").
 
 N > 1 (`--gpus N`: one process per GPU; started here through torch.distributed.run when no
@@ -63,7 +64,7 @@ def parse(argv=None):
                          "100 -> 50 + 50).  N>1 tiles: = --batch")
     ap.add_argument("--inflight", type=int, default=1,
                     help="launches in flight (a swap chain: one stream and one output buffer per slot).  1 (default): "
-                         "every launch is timed alone with a HIP event pair, so kernel time x launches <= wall time")
+                         "the launches run alone, back to back, so kernel time x launches <= wall time")
     ap.add_argument("--no-pipeline", action="store_true",
                     help="N>1: gather each frame before tracing the next (no double buffering)")
     ap.add_argument("--batch", type=int, default=0,
@@ -244,8 +245,11 @@ def measure_single(ctx, sc, args, torch, abi, steps, warmup):
             ctx.render_bands_batch(W, H, H, 0, 1, m, bufs[i].data_ptr(), W * H * 4, abi.RT_BANDS_INT32,
                                    streams[i].cuda_stream)
 
-    # one launch in flight: an event pair around every launch measures that launch alone
-    ctx.set_timing(1 if nf == 1 else 4)
+    # One launch in flight: no event pairs inside the timed region (each pair around a launch costs
+    # ~9 us of GPU time, tools/region_probe.py); the events around the region measure the launches,
+    # and an untimed pass of the same launches afterwards brackets each one (cross-check).
+    # Overlapping launches (--inflight > 1): a sampled pair per 4 launches.
+    ctx.set_timing(0 if nf == 1 else 4)
     t_w = time.perf_counter()
     issue(warmup)
     torch.cuda.synchronize()
@@ -258,8 +262,10 @@ def measure_single(ctx, sc, args, torch, abi, steps, warmup):
         done += n
         torch.cuda.synchronize()
     ctx.reset_stats()
-    torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)  # the first record of an event creates it (~10 us of host time): not in the region
+    ev1.record(stream)
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record(stream)  # on the launch stream(s): the others start after it, it ends after them
     for s in streams[1:]:
@@ -272,8 +278,18 @@ def measure_single(ctx, sc, args, torch, abi, steps, warmup):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     st = ctx.stats()
+    launch_s = None
+    if nf == 1:  # cross-check (untimed): the same launches, an event pair around each
+        ctx.set_timing(1)
+        ctx.reset_stats()
+        issue(steps)
+        torch.cuda.synchronize()
+        s2 = ctx.stats()
+        launch_s = s2["kernel_ms"] / 1e3 / s2["timed_launches"] if s2["timed_launches"] else None
+    ctx.set_timing(64)  # the library's default sampling
     return {"elapsed": elapsed, "period_s": ev0.elapsed_time(ev1) / 1e3 / steps, "stats": st, "host_s": host_s,
-            "launches": len(plan_launches(steps, fpl)), "warmup_effective": done, "inflight": nf}
+            "launches": len(plan_launches(steps, fpl)), "warmup_effective": done, "inflight": nf,
+            "launch_events_s": launch_s}
 
 
 def single_summary(sc, m, steps):
@@ -283,7 +299,10 @@ def single_summary(sc, m, steps):
     W, H = sc.width, sc.height
     launches = m["launches"]
     frames_per_launch = steps / launches
-    kernel_s = st["kernel_ms"] / 1e3 / max(1, st["timed_launches"]) if st["timed_launches"] else m["period_s"]
+    if m["inflight"] == 1:  # launches back to back on one stream: the region's events / launches
+        kernel_s = m["period_s"] * steps / launches
+    else:  # overlapping launches: the sampled per-launch event pairs
+        kernel_s = st["kernel_ms"] / 1e3 / max(1, st["timed_launches"]) if st["timed_launches"] else m["period_s"]
     achieved = 4.0 * W * H * frames_per_launch / kernel_s / 1e9
     return {
         "value": rays / m["elapsed"] / 1e6, "unit": "Mray/s", "ms_per_step": m["elapsed"] * 1e3 / steps,
@@ -292,6 +311,7 @@ def single_summary(sc, m, steps):
         else "trace_bundle_kernel",
         "kernel_avg_ms": kernel_s * 1e3, "kernel_ms_per_frame": kernel_s * 1e3 / frames_per_launch,
         "frames_per_launch": frames_per_launch, "launches": launches, "timed_launches": st["timed_launches"],
+        "kernel_avg_ms_launch_events": m["launch_events_s"] * 1e3 if m["launch_events_s"] else None,
         "frame_period_ms": m["period_s"] * 1e3, "hbm_gbs": achieved, "hbm_frac": achieved / HBM_PEAK_GBS,
         "f_alg": OPS_PER_SPHERE_TEST * st["sphere_tests"] + OPS_PER_PLANE_TEST * st["plane_tests"],
     }
@@ -494,8 +514,9 @@ def main():
             for _ in range(n):
                 step()
 
-    if launch_frames > 1:
-        ctx.set_timing(4)  # launches of many frames: an event pair per 4 launches costs nothing
+    # no event pairs around the launches of the timed region (each pair costs ~9 us of GPU time,
+    # tools/region_probe.py): the kernel duration comes from an untimed second pass (below)
+    ctx.set_timing(0)
     if tg is not None and not tg.idle and not tg.direct:
         # size the codec's scratch for a whole batch before anything is timed (rt_encode_bands grows
         # it on demand, behind a device synchronisation)
@@ -525,10 +546,12 @@ def main():
         if not args.no_speculate:
             tg.set_capacity()  # the warm-up's largest wire per frame x 1.25 (checked per batch)
 
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)  # the first record of an event creates it (~10 us of host time): not in the region
+    ev1.record(stream)
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(stream)  # on the launch stream(s): the others start after it, it ends after them
     for st_ in streams[1:]:
@@ -547,12 +570,26 @@ def main():
     st = ctx.stats()
     rays = st["primary_rays"] + st["reflect_rays"] + st["shadow_rays"]
     f_alg = OPS_PER_SPHERE_TEST * st["sphere_tests"] + OPS_PER_PLANE_TEST * st["plane_tests"]
-    # Kernel duration per launch: the library's sampled HIP event pairs on each launch's own
-    # stream (rt_set_timing; what rocprofv3's kernel trace reports too).  The frame period --
-    # HIP events around the timed region / steps -- is shorter when frames overlap.
-    sampled_s = st["kernel_ms"] / 1e3 / max(1, st["timed_launches"])
     period_s = ev0.elapsed_time(ev1) / 1e3 / args.steps
-    kernel_s = sampled_s if st["timed_launches"] else period_s
+    # what the JSON line reports of the timed run, read before the second pass below
+    gather_info = None
+    if tg is not None:
+        gather_info = {"bytes_sent": tg.bytes_sent, "speculative": tg.capacity_per_frame is not None,
+                       "redone": tg.redone}
+    verified = verify_rings(ctx, tg, W, H, args.steps, torch) if (args.verify and rank == 0) else None
+    # Kernel duration per launch: an untimed second pass of the same frames (same collectives on
+    # every rank) with a HIP event pair around every launch on its own stream (rt_set_timing 1;
+    # what rocprofv3's kernel trace reports too).  The frame period -- HIP events around the timed
+    # region / steps -- is shorter when frames overlap.
+    ctx.set_timing(1)
+    ctx.reset_stats()
+    run(args.steps)
+    finish()
+    torch.cuda.synchronize()
+    st2 = ctx.stats()
+    ctx.set_timing(64)  # the library's default sampling
+    sampled_s = st2["kernel_ms"] / 1e3 / max(1, st2["timed_launches"])
+    kernel_s = sampled_s if st2["timed_launches"] else period_s
     if distributed:
         t = torch.tensor([elapsed, float(rays), float(f_alg), kernel_s], dtype=torch.float64, device="cuda")
         tmax = t.clone()
@@ -609,8 +646,8 @@ def main():
                 "kernel": "trace_direct_kernel" if sc and len(sc.spheres) < 12 else "trace_bundle_kernel",
                 "kernel_avg_ms": kernel_s * 1e3,
                 "frames_per_launch": launch_frames,
-                "kernel_avg_source": "sampled per-launch HIP event pairs on the launch's stream (rt_set_timing: every "
-                                     "64th launch, every 4th for multi-frame launches)",
+                "kernel_avg_source": "an untimed second pass of the same run with a HIP event pair around every "
+                                     "launch on its stream (rt_set_timing 1), max over ranks",
                 "frame_period_ms": period_s * 1e3,
                 "note": "algorithmic bytes = 4 B framebuffer store per pixel x pixels per launch; the path is "
                         "FP32-VALU-bound",
@@ -639,14 +676,14 @@ def main():
         if args.rehearse_gloo:
             out["rehearsal"] = (f"gloo: {world} ranks sharing {torch.cuda.device_count()} GPU(s) -- a check of the N > 1 "
                                 f"code path, not a measurement")
-        if tg is not None:
+        if gather_info is not None:
             # wire bytes each rank shipped per frame (max over ranks, as gathered), vs the raw band set
-            out["config"]["gather_wire_bytes_per_frame"] = tg.bytes_sent / steps
+            out["config"]["gather_wire_bytes_per_frame"] = gather_info["bytes_sent"] / steps
             out["config"]["gather_rgb24_bytes_per_frame"] = 3 * rb.slot_elems
-            out["config"]["gather_speculative"] = tg.capacity_per_frame is not None
-            out["config"]["gather_redone_batches"] = tg.redone
+            out["config"]["gather_speculative"] = gather_info["speculative"]
+            out["config"]["gather_redone_batches"] = gather_info["redone"]
         if args.verify:
-            out["verified_frames"] = verify_rings(ctx, tg, W, H, args.steps, torch)
+            out["verified_frames"] = verified
         print(json.dumps(out), flush=True)
     ctx.close()
     if distributed:
@@ -695,7 +732,7 @@ def main_single(args, torch, Context, abi, scenes):
     valu_insts = (pmc.get("counters") or {}).get("SQ_INSTS_VALU") if pmc else None
     valu_frame = valu_insts / pmc_frames if valu_insts else None  # wave instructions per frame
     kernel_frame_s = r["kernel_ms_per_frame"] / 1e3
-    isolated = m["inflight"] == 1 and r["timed_launches"] == r["launches"]
+    isolated = m["inflight"] == 1
     out = {
         "metric": METRIC,
         "value": r["value"],
@@ -732,8 +769,11 @@ def main_single(args, torch, Context, abi, scenes):
             "launches": r["launches"],
             "kernel_ms_per_frame": r["kernel_ms_per_frame"],
             "frame_period_ms": r["frame_period_ms"],
-            "kernel_avg_source": ("HIP event pair around every launch on its stream, one launch in flight (the "
-                                  "launch alone on the GPU, as rocprofv3's kernel trace of the same command)")
+            "kernel_avg_ms_launch_events": r["kernel_avg_ms_launch_events"],
+            "kernel_avg_source": ("HIP events around the timed region on the launch stream / launches (one launch "
+                                  "in flight, launches back to back: the launches alone on the GPU, as rocprofv3's "
+                                  "kernel trace of the same command); kernel_avg_ms_launch_events = an untimed "
+                                  "second pass of the same launches with an event pair around each")
             if isolated else "sampled HIP event pairs of overlapping launches (--inflight > 1)",
             "note": "algorithmic bytes = 4 B framebuffer store per pixel x frames per launch; traffic = PMC "
                     "FETCH_SIZE x 2 + WRITE_SIZE per launch (profiles/pmc_traffic.json); the path is "

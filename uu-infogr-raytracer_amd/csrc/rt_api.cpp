@@ -122,6 +122,12 @@ struct rt_ctx {
     uint64_t timed[3] = {0, 0, 0};  // timed launches, copies, gathers
     int timing_every = 64;
     int32_t* host_staging = nullptr;
+    // view_params cache: the camera and frame size of the last call (this scene) and the view part
+    // of LaunchParams they gave (per-sphere screen boxes: a few us of host trig per launch)
+    bool view_ok = false;
+    rt_camera view_cam{};
+    int view_w = 0, view_h = 0;
+    LaunchParams view_lp{};
 };
 
 // ----------------------------------------------------------------------------
@@ -323,7 +329,24 @@ PrimBox prim_box(const LaunchParams& lp, const DevSphere& s) {
     return b;
 }
 
+void copy_view(const LaunchParams& from, LaunchParams& to) {
+    std::memcpy(to.cam, from.cam, sizeof to.cam);
+    std::memcpy(to.right, from.right, sizeof to.right);
+    std::memcpy(to.up, from.up, sizeof to.up);
+    std::memcpy(to.fwd, from.fwd, sizeof to.fwd);
+    to.pw = from.pw, to.ph = from.ph, to.nearc = from.nearc;
+    to.W = from.W, to.H = from.H;
+    to.prim_const = from.prim_const;
+    std::memcpy(to.pc, from.pc, sizeof to.pc);
+    std::memcpy(to.pbox, from.pbox, sizeof to.pbox);
+}
+
 int view_params(rt_ctx* ctx, int W, int H, LaunchParams& lp) {
+    if (ctx->view_ok && ctx->view_w == W && ctx->view_h == H &&
+        std::memcmp(&ctx->view_cam, &ctx->cam, sizeof ctx->cam) == 0) {
+        copy_view(ctx->view_lp, lp);
+        return RT_OK;
+    }
     rt_view v;
     int rc = rt_camera_view(&ctx->cam, W, H, &v);
     if (rc != RT_OK) return fail(ctx, rc, "invalid frame size %dx%d", W, H);
@@ -342,6 +365,8 @@ int view_params(rt_ctx* ctx, int W, int H, LaunchParams& lp) {
             lp.pc[i] = PrimConst{oc.x, oc.y, oc.z, hdot(oc, oc) - sph[i].r2};
             lp.pbox[i] = prim_box(lp, sph[i]);
         }
+    copy_view(lp, ctx->view_lp);
+    ctx->view_cam = ctx->cam, ctx->view_w = W, ctx->view_h = H, ctx->view_ok = true;
     return RT_OK;
 }
 
@@ -649,6 +674,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
     }
     ctx->layout = L;
     ctx->has_scene = true;
+    ctx->view_ok = false;
     return RT_OK;
 }
 
