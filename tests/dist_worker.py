@@ -157,7 +157,7 @@ def run_batched(rank, world, port, cfg, width, height, band_rows, frames, per_ba
 
 
 def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batch, result_path, rank0_codec=False,
-              compositor=False, speculate=0):
+              compositor=False, speculate=0, spec_after_drain=False):
     """bench.py's default N>1 step: F frames per batch, tile-encoded band sets (host mirror of
     rt_encode_bands), size all_reduce + gather, rank 0 decodes every frame (host mirror of
     rt_decode_gathered) and checks it against the oracle."""
@@ -186,25 +186,29 @@ def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batc
         brank, bworld = (max(0, rank - 1), world - 1) if compositor else (rank, world)
         rb = RowBands(width, height, band_rows, brank, bworld)
         got = {}
-        batch_of = []  # frame index of every decoded frame slot, in decode order
+        pending = {}  # batch -> (frame ring, frames) decoded, not yet read out of its ring
 
         def encode(raw, n, wire, size, _stream):
             b = tilecodec.encode(raw.numpy()[:n * rb.slot_elems], width, height, band_rows, brank, bworld, n)
             wire.numpy()[:len(b)] = np.frombuffer(b, dtype=np.uint8)
             size[0] = len(b)
 
-        decoded = [0]
-
         def decode(recv, rank_stride, n, frames_, _stream, first_rank):
+            # (a speculative batch that outgrew its gather is decoded twice: the later decode stands,
+            # so a batch's frames are read out of the ring only before the ring is rendered again)
             host = recv.numpy()
             fr = frames_.numpy().reshape(-1, height, width)
             for r in range(first_rank, bworld):
                 tilecodec.decode_into(fr[:n], host[r * rank_stride:(r + 1) * rank_stride], width, height,
                                       band_rows, r, bworld)
-            for f in range(n):
-                got[decoded[0] + f] = fr[f].copy()
-                fr[f] = -7  # the ring slot is reused: stale pixels must not pass
-            decoded[0] += n
+            pending[g.decode_batch] = (fr, n)
+
+        def read_out(upto):
+            for b in sorted(x for x in pending if x <= upto):
+                fr, n = pending.pop(b)
+                for f in range(n):
+                    got[b * g.F + f] = fr[f].copy()
+                    fr[f] = -7  # the ring slot is reused: stale pixels must not pass
 
         g = TileBandGather(rb, "cpu", per_batch, lambda n: tilecodec.layout(width, height, band_rows, bworld, n),
                            encode, decode, rank0_codec=rank0_codec, compositor=compositor, phys_rank=rank,
@@ -215,8 +219,11 @@ def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batc
         for k in range(frames):
             if k % g.F == 0:
                 if speculate and k == 2 * g.F:  # the sizes of the first batches are known by now
+                    if spec_after_drain:  # as bench.py: the warm-up drained, the pipeline is empty
+                        g.drain()
                     g.set_capacity(speculate)
                 g.begin_batch()
+                read_out(k // g.F - 3)  # this batch renders into the ring of batch b-3
             if g.idle:  # the compositor rank renders nothing
                 g.commit()
                 continue
@@ -233,6 +240,7 @@ def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batc
                     dst[l0 * width:(l0 + n) * width] = rows.reshape(-1)
             g.commit()
         g.drain()
+        read_out(frames)
         if speculate and speculate < 1:
             assert g.redone > 0, "a margin below 1 must force a gather at the real size"
         if rank == 0:

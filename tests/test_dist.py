@@ -126,24 +126,32 @@ def test_scatter_gathered_host_matches_scatter_host():
         assert np.array_equal(scatter_gathered_host(buf, stride, W, H, br, world, bpp), frame)
 
 
-@pytest.mark.parametrize("world,frames,per_batch,rank0_codec,compositor,speculate",
-                         [(2, 7, 3, False, False, 0), (3, 5, 2, False, False, 0), (2, 9, 2, False, False, 0),
-                          (3, 7, 3, True, False, 0), (3, 7, 3, False, True, 0), (4, 5, 2, False, True, 0),
-                          (2, 4, 4, False, True, 0), (2, 9, 2, False, False, 1.25), (3, 9, 2, False, True, 0.5),
-                          (2, 8, 2, True, False, 0.25)])
-def test_gloo_tile_encoded_gather(tmp_path, world, frames, per_batch, rank0_codec, compositor, speculate):
+@pytest.mark.parametrize("world,frames,per_batch,rank0_codec,compositor,speculate,after_drain",
+                         [(2, 7, 3, False, False, 0, False), (3, 5, 2, False, False, 0, False),
+                          (2, 9, 2, False, False, 0, False), (3, 7, 3, True, False, 0, False),
+                          (3, 7, 3, False, True, 0, False), (4, 5, 2, False, True, 0, False),
+                          (2, 4, 4, False, True, 0, False), (2, 9, 2, False, False, 1.25, False),
+                          (3, 9, 2, False, True, 0.5, False), (2, 8, 2, True, False, 0.25, False),
+                          (2, 5, 2, False, False, 0.25, True), (3, 9, 2, False, True, 1.25, True),
+                          (3, 9, 2, True, False, 0.5, True)])
+def test_gloo_tile_encoded_gather(tmp_path, world, frames, per_batch, rank0_codec, compositor, speculate,
+                                  after_drain):
     """bench.py's default N>1 step: tile-encoded band sets, size all_reduce + gather, three-stage
     pipeline; every frame decodes to its own oracle frame, the last batch may be partial.  With
     `compositor` (bench.py at N >= 8) rank 0 traces nothing and decodes every band set.  With
     `speculate`, after the first batch the gathers use speculative sizes (set_capacity(margin));
-    margins below 1 force batches to be gathered again at their reduced size."""
+    margins below 1 force batches to be gathered again at their reduced size.  With `after_drain`
+    the pipeline is drained before the switch (as bench.py's warm-up): the next batch finds it
+    empty and takes the gather-first path (decode before the size check, a second gather and
+    decode when the guess was short); with 5 frames in batches of 2 that batch is the last,
+    partial one, as in a short run."""
     import dist_worker
     ctx = mp.get_context("spawn")
     port = _free_port()
     result = tmp_path / "result.txt"
     procs = [ctx.Process(target=dist_worker.run_tiles,
                          args=(r, world, port, "C3", 43, 29, 4, frames, per_batch, str(result), rank0_codec,
-                               compositor, speculate))
+                               compositor, speculate, after_drain))
              for r in range(world)]
     for p in procs:
         p.start()

@@ -137,15 +137,22 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("extra", [["--rank0-codec"], []])
-def test_tile_pipeline_on_cuda_streams(extra):
+@pytest.mark.parametrize("extra,shape", [(["--rank0-codec"], "small"), ([], "small"),
+                                         (["--rank0-codec"], "full"), (["--rank0-codec"], "short")])
+def test_tile_pipeline_on_cuda_streams(extra, shape):
     """bench.py's N>1 tile pipeline (encode, size all_reduce, gather, decode on side streams,
     event-ordered buffer reuse) with a real RCCL process group of one rank: rank 0 checks every
-    frame left in its rings against a single-launch render (--verify, exit 3 on a mismatch)."""
+    frame left in its rings against a single-launch render (--verify, exit 3 on a mismatch).
+    "full": 1080p C2, 300 frames in batches of 64 with speculative gather sizes -- the shape that
+    exposed speculative gathers not ordered after their encode (fixed by an encode event);
+    "short": the driver's 20 frames, one batch through the gather-first path."""
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     env.pop("WORLD_SIZE", None)
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--dist-path", "--config", "C2", "--size", "640x360",
-           "--steps", "40", "--warmup", "16", "--batch", "8", "--verify", "--no-cpu-baseline"] + extra
+    size = {"small": ["--size", "640x360", "--steps", "40", "--warmup", "16", "--batch", "8"],
+            "full": ["--steps", "300", "--warmup", "64"],
+            "short": ["--steps", "20", "--warmup", "5"]}[shape]
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--dist-path", "--config", "C2", "--verify",
+           "--no-cpu-baseline"] + size + extra
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-2000:]
     import json

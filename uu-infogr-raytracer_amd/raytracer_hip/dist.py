@@ -253,6 +253,15 @@ class TileBandGather:
     decode b-3 filled it -- `begin_batch`).  With gloo on CPU tensors (tests) the same
     sequence runs synchronously.
 
+    Speculative mode (`set_capacity`, bench.py after its warm-up): a batch's gather size is a
+    guess (1.25 x the largest wire per frame so far), so stage B gathers without waiting for the
+    size, and stage C checks the reduced size before the decode; a batch whose largest wire
+    outgrew the guess is gathered again in full (every rank sees the same reduced size, so all of
+    them take part).  A batch that finds the pipeline empty (a run's first batch -- all of a
+    short run) goes further: its gather is issued in stage A right behind the encode, the size
+    reduce after it, and stage C decodes before it reads the size (decoding again after a second
+    gather), so neither the reduce nor the host's read-back sits between encode and decode.
+
         g.begin_batch(streams)      -> before frame k when k % F == 0 (rank 0: ring reuse)
         dst = g.target(k)           -> rank 0 direct: int32 view of frame k's ring slot (render
                                        its bands there, RT_BANDS_FRAME); else this rank's raw
@@ -310,6 +319,7 @@ class TileBandGather:
         self.batch = 0         # batches encoded
         self.stage_b = []      # [(batch, n_frames, all_reduce work)]
         self.stage_c = []      # [(batch, n_frames, gather work)]
+        self.encoded_ev = {}   # batch -> event after its encode on the main stream (wire ready)
         self.gathered_ev = {}  # batch -> event after its gather (wire reusable)
         self.decoded_ev = {}   # batch -> event after its decode (receive buffer / frame ring reusable)
         self.decoded = 0       # batches decoded (rank 0)
@@ -317,15 +327,18 @@ class TileBandGather:
         self.max_per_frame = 0.0  # largest reduced wire size / frames of a batch seen so far
         self.capacity_per_frame = None  # speculative gather size (set_capacity); None = wait for the size
         self.redone = 0        # batches whose wire outgrew the speculative size (gathered again)
+        self.decode_batch = -1  # the batch of the decode being issued
 
     def set_capacity(self, margin=1.25):
         """From now on gather each batch with a speculative size -- `margin` x the largest wire per
         frame seen so far (every rank holds the same all-reduced sizes, so they agree without
-        communicating) -- issued right after the size reduce instead of after the host has read
-        the reduced size back.  The reduced size is still checked before the batch is decoded: a
-        batch whose largest wire exceeded the speculative size is gathered again at its real size
-        (every rank takes the same decision from the same reduced value)."""
+        communicating) -- issued right behind the encode, before the size reduce.  The reduced size
+        is checked after the batch's decode was issued: a batch whose largest wire exceeded the
+        speculative size is gathered again at its real size and decoded again (every rank takes
+        the same decision from the same reduced value)."""
         if self.max_per_frame > 0:
+            while self.stage_b:  # batches whose size reduce is out: gathered at their real size first
+                self._stage_b()
             self.capacity_per_frame = self.max_per_frame * margin
 
     def _read_size(self, i, work):
@@ -342,18 +355,26 @@ class TileBandGather:
             self.size_host[i] = self.size[i][0]
         return (int(self.size_host[i]) + 7) // 8 * 8
 
-    def _gather(self, b, i, n):
+    def _gather(self, b, i, n, reader=None):
+        """Gather n bytes of every rank's wire i into receive buffer b % 2, after batch b's encode
+        and after the decode of batch `reader` (default b-2, the buffer's previous batch) has read
+        that buffer."""
         import torch
         import torch.distributed as dist
         j = b % 2
+        reader = b - 2 if reader is None else reader
         glist = None
         if self.root:
             slot = [(r - 1) % self.pworld if self.compositor else r for r in range(self.pworld)]
             glist = [self.recv[j][q * self.rank_stride:q * self.rank_stride + n] for q in slot]
         if self.cuda:
             with torch.cuda.stream(self.comm):
-                if b - 2 in self.decoded_ev:  # receive buffer j was last read by decode b-2
-                    self.comm.wait_event(self.decoded_ev[b - 2])
+                # The gather is issued on `comm`, which ProcessGroupNCCL orders it after: wire i
+                # must be encoded (a speculative gather is issued without waiting for the size
+                # reduce, so nothing else orders it after the encode)
+                self.comm.wait_event(self.encoded_ev[b])
+                if reader in self.decoded_ev:  # receive buffer j was last read by that decode
+                    self.comm.wait_event(self.decoded_ev[reader])
                 for old in [x for x in self.decoded_ev if x < b - 4]:
                     del self.decoded_ev[old]
                 return dist.gather(self.wire[i][:n], glist, dst=0, async_op=True)
@@ -389,6 +410,13 @@ class TileBandGather:
                 st.wait_event(ev)
 
     # -- stages -------------------------------------------------------------------
+    def _spec_bytes(self, n_frames):
+        """Speculative gather size of a batch: capacity per frame x frames, at least the wire's fixed
+        part (headers: a decode of a wire cut short then reads only stale payload, inside the slot)."""
+        n = int(self.capacity_per_frame * n_frames)
+        n = max(n, int(self.layout_fn(n_frames).fixed_bytes))
+        return min(self.rank_stride, (n + 7) // 8 * 8)
+
     def _stage_a(self, main, n_frames):
         import torch.distributed as dist
         b = self.batch
@@ -397,6 +425,8 @@ class TileBandGather:
             self._stage_b()
         while self.stage_c and self.stage_c[0][0] <= b - 3:
             self._stage_c()
+        # an empty pipeline (a run's first batch; all of a short run): speculative gather first
+        first = self.capacity_per_frame is not None and not self.stage_b and not self.stage_c
         if b - 3 in self.gathered_ev:  # wire i was last read by gather b-3
             ev = self.gathered_ev.pop(b - 3)
             if self.cuda:
@@ -405,8 +435,24 @@ class TileBandGather:
             self.size[i].zero_()  # nothing to ship: rank 0's bands are in its frames (or it has none)
         else:
             self.encode(self.raw[b % 2], n_frames, self.wire[i], self.size[i], main)
-        work = dist.all_reduce(self.size[i], op=dist.ReduceOp.MAX, async_op=True)
-        self.stage_b.append((b, n_frames, work))
+        if self.cuda:
+            import torch
+            ev = torch.cuda.Event()
+            ev.record(main)
+            self.encoded_ev[b] = ev
+            for old in [x for x in self.encoded_ev if x < b - 3]:
+                del self.encoded_ev[old]
+        if first:
+            # the gather right behind the encode and the size reduce after it, so that neither the
+            # reduce nor its read-back sits between the encode and the decode: stage C decodes, then
+            # checks the reduced size (and gathers + decodes again if it was exceeded)
+            n = self._spec_bytes(n_frames)
+            gw = self._gather(b, i, n)
+            work = dist.all_reduce(self.size[i], op=dist.ReduceOp.MAX, async_op=True)
+            self.stage_c.append((b, n_frames, gw, (work, n, True)))
+        else:
+            work = dist.all_reduce(self.size[i], op=dist.ReduceOp.MAX, async_op=True)
+            self.stage_b.append((b, n_frames, work))
         self.batch += 1
     def _stage_b(self):
         b = self.stage_b[0][0]
@@ -415,9 +461,10 @@ class TileBandGather:
         b, n_frames, work = self.stage_b.pop(0)
         i = b % 3
         if self.capacity_per_frame is not None:
-            # speculative size: gather now, check the reduced size in stage C
-            n = min(self.rank_stride, (int(self.capacity_per_frame * n_frames) + 7) // 8 * 8)
-            self.stage_c.append((b, n_frames, self._gather(b, i, n), (work, n)))
+            # speculative size: gather now, check the reduced size in stage C (before the decode:
+            # by then the reduce has long completed)
+            n = self._spec_bytes(n_frames)
+            self.stage_c.append((b, n_frames, self._gather(b, i, n), (work, n, False)))
             return
         n = self._read_size(i, work)
         self.max_per_frame = max(self.max_per_frame, n / n_frames)
@@ -425,17 +472,31 @@ class TileBandGather:
         self.stage_c.append((b, n_frames, self._gather(b, i, n), None))
 
     def _stage_c(self):
-        import torch
         b, n_frames, gw, spec = self.stage_c.pop(0)
-        if spec is not None:  # speculative gather: the reduced size decides whether it sufficed
-            work, n_spec = spec
-            n = self._read_size(b % 3, work)  # (reduced before the gather was issued)
+        if spec is None:
+            self._decode(b, n_frames, gw)
+        else:  # speculative gather: the reduced size decides whether it sufficed
+            work, n_spec, decode_first = spec
+            if decode_first:  # (a wire cut short decodes stale payload bytes inside its own slot)
+                self._decode(b, n_frames, gw)
+            n = self._read_size(b % 3, work)
             self.max_per_frame = max(self.max_per_frame, n / n_frames)
             self.bytes_sent += n_spec
             if n > n_spec:  # some wire outgrew it (every rank sees the same n): gather again, in full
-                self.redone += 1  # (collectives of one group run in issue order)
-                gw = self._gather(b, b % 3, n)
+                self.redone += 1  # (after a decode that read the buffer; collectives run in issue order)
+                gw = self._gather(b, b % 3, n, reader=b if decode_first else None)
                 self.bytes_sent += n
+            if n > n_spec or not decode_first:
+                self._decode(b, n_frames, gw)
+        if self.root:
+            self.decoded += 1
+
+    def _decode(self, b, n_frames, gw):
+        """Rank 0: after gather `gw`, decode batch b's wires into frame ring b % 3 (on `dec`).  A
+        speculative batch that outgrew its gather is decoded twice; the second decode is the one
+        that stands (`decode_batch` names the batch being decoded)."""
+        import torch
+        self.decode_batch = b
         if self.cuda:
             with torch.cuda.stream(self.dec):
                 gw.wait()
@@ -454,8 +515,6 @@ class TileBandGather:
             if self.root:
                 self.decode(self.recv[b % 2], self.rank_stride, n_frames, self.ring_of(b), None, self.first_rank)
                 self.decoded_ev[b] = None
-        if self.root:
-            self.decoded += 1
 
     def commit(self, main=None):
         """Frame k traced (on `main`'s stream or joined into it).  At a batch end: stages A, B, C."""
