@@ -918,22 +918,38 @@ template <bool PRIMARY, bool A2OK, typename T>
 __device__ __forceinline__ void bundle_candidates(const LaunchParams& p, unsigned long long m, int base, f3 o, f3 d,
                                                   float a2, float a4, bool a2_ok, bool active, float& best_s,
                                                   int& win_s, T& tl) {
-    while (m) {
-        const int i = base + (int)__builtin_ctzll(m);
-        m &= m - 1;
-        tl.sphere(active);
-        float t;
+    auto test = [&](int i) -> float {
         if (PRIMARY && p.prim_const) {
             // o == camera: oc = cam - c and c = oc.oc - r^2 are per-frame constants (:614-619)
             const PrimConst pc = p.pc[i];
             const float b = 2.0f * dot(mk(pc.ocx, pc.ocy, pc.ocz), d);
             const float disc = b * b - a4 * pc.c;
-            t = A2OK ? root_t1(b, disc, a2) : (a2_ok ? root_t1(b, disc, a2) : root_full(b, disc, a2));
-        } else {
-            t = sphere_t<A2OK>(o, d, a2, a4, a2_ok, p.sph[i]);
+            return A2OK ? root_t1(b, disc, a2) : (a2_ok ? root_t1(b, disc, a2) : root_full(b, disc, a2));
         }
+        return sphere_t<A2OK>(o, d, a2, a4, a2_ok, p.sph[i]);
+    };
+    auto take = [&](float t, int i) {
         if (PRIMARY) take_primary(t, i, best_s, win_s);
         else take_secondary(t, i, best_s, win_s);
+    };
+    // two candidates per iteration: independent sqrt chains (ILP), selections in ascending order;
+    // an odd last candidate alone (C4 -0.9 %, C5 -1.2 %; testing it twice instead: -0.5 / -0.7 %,
+    // profiles/ab/r02_near_pairs.txt)
+    while (m) {
+        const int i0 = base + (int)__builtin_ctzll(m);
+        m &= m - 1;
+        if (m) {
+            const int i1 = base + (int)__builtin_ctzll(m);
+            m &= m - 1;
+            tl.sphere(active);
+            tl.sphere(active);
+            const float t0 = test(i0), t1 = test(i1);
+            take(t0, i0);
+            take(t1, i1);
+        } else {
+            tl.sphere(active);
+            take(test(i0), i0);
+        }
     }
 }
 

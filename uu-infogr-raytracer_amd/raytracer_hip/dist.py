@@ -315,6 +315,7 @@ class TileBandGather:
                         for _ in range(3)] if self.root else None)
         if self.cuda:
             self.comm, self.dec = torch.cuda.Stream(self.device), torch.cuda.Stream(self.device)
+            self.enc_events = [torch.cuda.Event() for _ in range(4)]
         self.k = 0             # frames rendered
         self.batch = 0         # batches encoded
         self.stage_b = []      # [(batch, n_frames, all_reduce work)]
@@ -435,9 +436,8 @@ class TileBandGather:
             self.size[i].zero_()  # nothing to ship: rank 0's bands are in its frames (or it has none)
         else:
             self.encode(self.raw[b % 2], n_frames, self.wire[i], self.size[i], main)
-        if self.cuda:
-            import torch
-            ev = torch.cuda.Event()
+        if self.cuda:  # (events reused round robin: a wait takes the state recorded before it)
+            ev = self.enc_events[b % len(self.enc_events)]
             ev.record(main)
             self.encoded_ev[b] = ev
             for old in [x for x in self.encoded_ev if x < b - 3]:
