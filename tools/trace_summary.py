@@ -2,11 +2,13 @@
 bench.py's roofline.kernel_avg_ms (HIP events around the timed launches of the same process).
 
     python tools/trace_summary.py TRACE_DIR_OR_CSV [--kernel trace_direct_kernel] [--last 16]
-                                  [--bench bench_line.json]
+                                  [--skip-last 16] [--bench bench_line.json]
 
 Prints the average over every dispatch of the kernel (the kernel_stats.csv figure) and over the
 last `--last` dispatches (the bench's timed launches: warm-up and clock-ramp launches come first),
-and, with --bench, the bench line's kernel_avg_ms and their ratio."""
+and, with --bench, the bench line's kernel_avg_ms and their ratio.  --skip-last N leaves out the
+trailing N dispatches first: bench.py's untimed second pass of the same launches (each with its
+own event pair, roofline.kernel_avg_ms_launch_events), reported separately."""
 import argparse
 import csv
 import glob
@@ -19,6 +21,7 @@ def main():
     ap.add_argument("path")
     ap.add_argument("--kernel", default="rtk::trace_")
     ap.add_argument("--last", type=int, default=0)
+    ap.add_argument("--skip-last", type=int, default=0)
     ap.add_argument("--bench", default="")
     a = ap.parse_args()
     fn = a.path if a.path.endswith(".csv") else glob.glob(os.path.join(a.path, "**", "*kernel_trace.csv"),
@@ -28,6 +31,11 @@ def main():
     names = sorted({r["Kernel_Name"] for r in rows})
     dur = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows]  # ms
     print(f"kernel(s): {'; '.join(names)}")
+    if a.skip_last:
+        tail = dur[-a.skip_last:]
+        dur = dur[:-a.skip_last]
+        print(f"trailing {len(tail)} dispatches (bench.py's untimed per-launch-event pass): average "
+              f"{sum(tail) / len(tail):.4f} ms -- left out below")
     print(f"dispatches {len(dur)}: average {sum(dur) / len(dur):.4f} ms (all)")
     out = {"kernels": names, "dispatches": len(dur), "avg_ms_all": sum(dur) / len(dur)}
     if a.last:
