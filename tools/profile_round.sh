@@ -3,7 +3,8 @@
 # gpurun_out/pmc_traffic.json; then the bench line of the config under
 # rocprofv3 --kernel-trace --stats (the same process: its kernel_avg_ms and the trace's average
 # duration of the trace kernel describe the same launches; no Tick probe, no work count, so
-# every dispatch of that kernel is a bench launch).
+# every dispatch of that kernel is a bench launch: warm-up, the 16 timed launches, then the 16 of
+# bench.py's untimed per-launch-event pass), reconciled by tools/trace_summary.py.
 #   bash tools/profile_round.sh C2 C3 C4 C5
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -21,4 +22,6 @@ for cfg in "$@"; do
         > "gpurun_out/trace_bench_$cfg.json" 2> "gpurun_out/trace_$cfg.log"
     rc=$?; echo "trace $cfg rc=$rc: $(tail -c 200 gpurun_out/trace_bench_$cfg.json)"; [ $rc -eq 0 ] || exit $rc
     find "gpurun_out/trace_$cfg" -name "*kernel_stats.csv" -exec cp {} "gpurun_out/trace_${cfg}_kernel_stats.csv" \;
+    python3 tools/trace_summary.py "gpurun_out/trace_$cfg" --last 16 --skip-last 16 \
+        --bench "gpurun_out/trace_bench_$cfg.json" > "gpurun_out/trace_${cfg}_reconcile.txt"
 done
