@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 5
+#define RT_ABI_VERSION 6
 
 /* ---- status codes ---------------------------------------------------------- */
 enum {
@@ -239,14 +239,15 @@ int rt_scatter_gathered(rt_ctx* ctx, int width, int height, int band_rows, int w
                         const void* d_gathered, size_t slot_bytes, int format, int32_t* d_frame,
                         void* hip_stream);
 
-/* ---- tile codec for the gather to rank 0 (ABI 4) ------------------
+/* ---- tile codec for the gather to rank 0 (ABI 4, format 2 since ABI 6) --
  * Lossless: each rank encodes its int32 band sets (as rt_render_bands writes them, the
- * slot of the largest band set per frame) into a "wire" -- per 8x8 tile a raw first pixel,
- * left/above prediction, zigzag residuals as w-bit planes (one wave ballot each) -- and rank
- * 0 decodes all ranks' wires straight into the frames.  Rendered frames are mostly flat, so
- * the wire is ~7-11x smaller than RGB24 at 1080p; the format is specified
- * in raytracer_hip/tilecodec.py.  The wire's size varies: the fixed part (header, tile
- * headers, chunk bases) is the same on every rank, the payload follows it. */
+ * slot of the largest band set per frame) into a "wire" -- per 8x8 tile a 4-byte header (raw
+ * first pixel, width code), second-difference (gradient) prediction, zigzag residuals packed
+ * at 0/2/3/4/6/8 bits per channel -- and rank 0 decodes all ranks' wires straight into the
+ * frames.  Rendered frames are mostly flat, so the wire is ~8-13x smaller than RGB24 at 1080p
+ * (DESIGN.md 1e); the format is specified in raytracer_hip/tilecodec.py.  The wire's size
+ * varies: the fixed part (header, tile headers, chunk bases) is the same on every rank, the
+ * payload follows it. */
 typedef struct rt_wire_layout {
     uint64_t fixed_bytes;  /* header + tile headers + chunk bases (8-aligned)          */
     uint64_t max_bytes;    /* fixed_bytes + the largest possible payload (capacity)     */

@@ -79,7 +79,7 @@ def test_top_byte_is_ignored():
 
 def test_compression_on_rendered_frames():
     """The point of the codec: rendered frames are mostly flat (small frames less so; C2 at
-    1920x1080 compresses 9.0x)."""
+    1920x1080 compresses 12.9x)."""
     for name, floor in (("frame_C2_96x54", 1.5), ("frame_REF_128", 1.5)):
         img = np.load(os.path.join(GOLDEN, name + ".npy")).astype(np.int32)
         H, W = img.shape

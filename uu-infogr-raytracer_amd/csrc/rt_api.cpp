@@ -852,7 +852,7 @@ static bool codec_geom(int width, int height, int band_rows, int world, int n_fr
     g = rtk::CodecGeom{};
     g.W = width, g.H = height, g.band_rows = band_rows, g.world = world;
     g.tiles_x = (int)tx, g.tiles_y = (int)ty, g.tiles_per_frame = (int)tpf, g.n_tiles = (int)nt, g.n_chunks = (int)nc;
-    g.fixed_bytes = ((size_t)16 + 8 * (size_t)nt + 4 * (size_t)nc + 7) / 8 * 8;
+    g.fixed_bytes = ((size_t)16 + 4 * (size_t)nt + 4 * (size_t)nc + 7) / 8 * 8;  // header, tile headers, chunk bases
     if (lay) {
         lay->fixed_bytes = g.fixed_bytes;
         lay->max_bytes = g.fixed_bytes + 8 * 24 * (size_t)nt;

@@ -4,20 +4,21 @@
 // the trace, bounds strong scaling.  Each rank encodes its band sets before
 // the gather and rank 0 decodes them straight into the frame.  The format is specified, and
 // mirrored on the host, in raytracer_hip/tilecodec.py.  In short, per 8x8 tile of a band set
-// (lane l = ry*8 + rx of one wave64): pixel (0,0) raw in the tile header; every other pixel
-// predicted by its left neighbour, the first column by the pixel above (odd rows) or by the
-// tile's first pixel (even rows) -- predictors a DPP row shift or a scalar can deliver; per
-// channel residuals mod 256, zigzag; widths rounded up to 0/1/2/4/8 bits, lane-packed.
-// Tiles are grouped in chunks of 8; a tile's payload lives at its chunk's base + its offset
-// inside the chunk.
+// (lane l = ry*8 + rx): pixel (0,0) raw in the tile's 4-byte header beside its width code;
+// per channel mod 256 the second differences r = dx - dx(row above), dx = p - p(left) (column 0:
+// p - p(0,0); row 0: r = dx) -- decoded by a prefix sum over the rows (3 DPP steps across the
+// tile's lanes) and one along each row (registers); zigzag; widths rounded up to 0/2/3/4/6/8
+// bits, lane-packed.  Tiles are grouped in chunks of 8; a tile's payload lives at its chunk's
+// base + the units of the chunk's earlier tiles (a wave scan of the headers).
 //
 // Encode = two launches per batch of frames (deterministic layout, no atomics), chunks of 8
 // tiles = one wave's, contiguous ranges of chunks per workgroup:
 //   encode_tiles_kernel  residuals, widths, packed segments (into the context's staging slot
-//                        of 48 words per tile, final byte layout), chunk-relative offsets ->
-//                        tile headers; chunk totals -> chunk_base[], range totals -> wg_total[]
+//                        of 48 words per tile, final byte layout), tile headers; chunk totals
+//                        -> chunk_base[], range totals -> wg_total[]
 //   encode_copy_kernel   range base = sum of the earlier ranges' totals, chunk bases by an LDS
-//                        scan, staged segments -> compact offsets; wire header and size
+//                        scan, staged segments -> compact offsets (chunk-relative offsets by a
+//                        wave scan of the headers); wire header and size
 // Decode = one launch for every rank's wire of a batch (decode_tiles_kernel).
 // Integer/byte work: the encoder reads each band-set pixel once (4 B), the decoder writes
 // each frame pixel once (4 B); both are instruction-lean (DPP row shifts, ballots, inverse
@@ -46,10 +47,10 @@ __device__ __forceinline__ int wave_index() { return __builtin_amdgcn_readfirstl
 __device__ __forceinline__ const uint32_t* wire_tile_hdr(const unsigned char* w) { return (const uint32_t*)(w + 16); }
 __device__ __forceinline__ uint32_t* wire_tile_hdr(unsigned char* w) { return (uint32_t*)(w + 16); }
 __device__ __forceinline__ uint32_t* wire_chunk_base(unsigned char* w, const CodecGeom& g) {
-    return (uint32_t*)(w + 16 + 8 * (size_t)g.n_tiles);
+    return (uint32_t*)(w + 16 + 4 * (size_t)g.n_tiles);
 }
 __device__ __forceinline__ const uint32_t* wire_chunk_base(const unsigned char* w, const CodecGeom& g) {
-    return (const uint32_t*)(w + 16 + 8 * (size_t)g.n_tiles);
+    return (const uint32_t*)(w + 16 + 4 * (size_t)g.n_tiles);
 }
 __device__ __forceinline__ uint64_t* wire_payload(unsigned char* w, const CodecGeom& g) {
     return (uint64_t*)(w + g.fixed_bytes);
@@ -115,8 +116,18 @@ __device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
     return x;
 }
 
-__device__ __forceinline__ uint32_t bitlen8(uint32_t v) { return v ? 32u - (uint32_t)__builtin_clz(v) : 0u; }
 __device__ __forceinline__ uint32_t units_of(uint32_t wm) { return (wm & 15u) + ((wm >> 4) & 15u) + ((wm >> 8) & 15u); }
+// Widths WIDTHS = {0, 2, 3, 4, 6, 8} by index (nibbles of 0x864320); a tile's width code is
+// i_R + 6 i_G + 36 i_B (< 216, the header's top byte).
+__device__ __forceinline__ uint32_t width_at(uint32_t i) { return (0x864320u >> (4u * i)) & 15u; }
+// widths of a code as wm = w_R | w_G << 4 | w_B << 8
+__device__ __forceinline__ uint32_t widths_of_code(uint32_t code) {
+    return width_at(code % 6u) | (width_at(code / 6u % 6u) << 4) | (width_at(code / 36u) << 8);
+}
+// Width index of a channel: bit length of its OR of zigzag residuals rounded up to a width.
+__device__ __forceinline__ uint32_t width_index(uint32_t o) {
+    return o == 0 ? 0u : o < 4 ? 1u : o < 8 ? 2u : o < 16 ? 3u : o < 64 ? 4u : 5u;
+}
 
 // Local row r of band set `rank` -> frame row.
 __device__ __forceinline__ int frame_row(const CodecGeom& g, int rank, int r) {
@@ -145,11 +156,6 @@ __device__ __forceinline__ TilePos tile_pos(const CodecGeom& g, int t0, int j) {
         if (++p.tr == g.tiles_y) p.tr = 0, ++p.f;
     }
     return p;
-}
-
-// Width of a channel: bit length of its OR rounded up to 0, 1, 2, 4 or 8.
-__device__ __forceinline__ uint32_t width_of(uint32_t o) {
-    return o == 0 ? 0u : o < 2 ? 1u : o < 4 ? 2u : o < 16 ? 4u : 8u;
 }
 
 // Encode one group of CODEC_TPW tiles (one chunk): tile headers with chunk-relative offsets,
@@ -195,43 +201,35 @@ __device__ __forceinline__ uint32_t encode_group(unsigned char* __restrict__ wir
     const bool live = t < g.n_tiles;
     const int ncols = e.ncols;
     const uint32_t* p = e.p;
-    // residuals: left neighbour; first column: above (odd rows) or the tile's first pixel
+    // residuals: second differences (dx along the row, column 0 against the tile's first pixel;
+    // then minus the row above's dx, rows >= 1)
     const uint32_t first = RT_ENC_DPP ? group8_first(p[0]) : (uint32_t)__shfl((int)p[0], lane & ~7, 64);
-    const uint32_t above = row_shr<1>(p[0]);
     uint32_t z[8];
-    z[0] = ncols > 0 ? zigzag_bytes(sub_bytes(p[0], (ry & 1) ? above : first)) & 0xffffffu : 0u;
 #pragma unroll
-    for (int rx = 1; rx < 8; ++rx) z[rx] = rx < ncols ? zigzag_bytes(sub_bytes(p[rx], p[rx - 1])) & 0xffffffu : 0u;
-    // tile OR of residuals -> widths (lane 8j+7 accumulates lanes 8j..8j+7), broadcast
+    for (int rx = 0; rx < 8; ++rx) {
+        const uint32_t dx = sub_bytes(p[rx], rx ? p[rx - 1] : first);
+        const uint32_t above = row_shr<1>(dx);  // (lane - 1 = the row above for ry >= 1)
+        const uint32_t r = ry ? sub_bytes(dx, above) : dx;
+        z[rx] = rx < ncols ? zigzag_bytes(r) & 0xffffffu : 0u;
+    }
+    // tile OR of residuals -> width indices, broadcast over the tile's lanes
     uint32_t o = z[0] | z[1] | z[2] | z[3] | z[4] | z[5] | z[6] | z[7];
-    uint32_t wm, incl, rel;
     if constexpr (RT_ENC_DPP) {
         o = group8_or(o);
-        wm = width_of((o >> 16) & 0xffu) | (width_of((o >> 8) & 0xffu) << 4) | (width_of(o & 0xffu) << 8);
-        if (!live) wm = 0;
-        // chunk-relative offsets: with each group's units in its lane 8j+7 only, the inclusive
-        // scan at lanes 8j..8j+6 is already the sum over the groups before j
-        const uint32_t u7 = ry == 7 ? units_of(wm) : 0u;
-        incl = wave_scan_incl(u7);
-        rel = incl - u7;
     } else {
         o |= row_shr<1>(o);
         o |= row_shr<2>(o);
         o |= row_shr<4>(o);
-        wm = width_of((o >> 16) & 0xffu) | (width_of((o >> 8) & 0xffu) << 4) | (width_of(o & 0xffu) << 8);
-        wm = (uint32_t)__shfl((int)wm, lane | 7, 64);
-        if (!live) wm = 0;
-        const uint32_t u = units_of(wm);
-        // chunk-relative offsets: inclusive scan over the group leaders (lanes 8j+7)
-        incl = ry == 7 ? u : 0u;
-#pragma unroll
-        for (int k = 8; k < 64; k <<= 1) {
-            const uint32_t x = (uint32_t)__shfl_up((int)incl, k, 64);
-            if (lane >= k) incl += x;
-        }
-        rel = (uint32_t)__shfl((int)(incl - u), lane | 7, 64);
+        o = (uint32_t)__shfl((int)o, lane | 7, 64);
     }
-    if (live && ry == 0) ((uint2*)wire_tile_hdr(wire))[t] = make_uint2(first, wm | (rel << 12));
+    const uint32_t iR = width_index((o >> 16) & 0xffu), iG = width_index((o >> 8) & 0xffu),
+                   iB = width_index(o & 0xffu);
+    const uint32_t code = live ? iR + 6u * iG + 36u * iB : 0u;
+    const uint32_t wm = live ? width_at(iR) | (width_at(iG) << 4) | (width_at(iB) << 8) : 0u;
+    // chunk total: with each group's units in its lane 8j+7 only, an inclusive wave scan
+    const uint32_t u7 = ry == 7 ? units_of(wm) : 0u;
+    const uint32_t incl = wave_scan_incl(u7);
+    if (live && ry == 0) wire_tile_hdr(wire)[t] = first | (code << 24);
     const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     if (lane == 63) wire_chunk_base(wire, g)[chunk] = total;  // chunk total, scanned later
     // segments: this row's residuals of channel c = bytes [ry*w, ry*w + w) of the segment
@@ -241,18 +239,25 @@ __device__ __forceinline__ uint32_t encode_group(unsigned char* __restrict__ wir
         for (int c = 0; c < 3; ++c) {
             const uint32_t w = (wm >> (4 * c)) & 15u;
             const int sh = 16 - 8 * c;
-            uint32_t lo = 0, hi = 0;
+            uint64_t acc = 0;
 #pragma unroll
-            for (int rx = 0; rx < 8; ++rx) {
-                const uint32_t v = (z[rx] >> sh) & 0xffu, pos = (uint32_t)rx * w;
-                if (pos < 32) lo |= v << pos;
-                else hi |= v << (pos - 32);
-            }
+            for (int rx = 0; rx < 8; ++rx) acc |= (uint64_t)((z[rx] >> sh) & 0xffu) << (rx * w);
             unsigned char* dst = seg + ry * w;
-            if (w == 8) *(uint2*)dst = make_uint2(lo, hi);
-            else if (w == 4) *(uint32_t*)dst = lo;
-            else if (w == 2) *(uint16_t*)dst = (uint16_t)lo;
-            else if (w == 1) *dst = (unsigned char)lo;
+            if (w == 8) {
+                *(uint64_t*)dst = acc;
+            } else if (w == 4) {
+                *(uint32_t*)dst = (uint32_t)acc;
+            } else if (w == 2) {
+                *(uint16_t*)dst = (uint16_t)acc;
+            } else if (w == 6) {  // 6 ry: 2-byte aligned
+                ((uint16_t*)dst)[0] = (uint16_t)acc;
+                ((uint16_t*)dst)[1] = (uint16_t)(acc >> 16);
+                ((uint16_t*)dst)[2] = (uint16_t)(acc >> 32);
+            } else if (w == 3) {
+                dst[0] = (unsigned char)acc;
+                dst[1] = (unsigned char)(acc >> 8);
+                dst[2] = (unsigned char)(acc >> 16);
+            }
             seg += 8 * w;
         }
     }
@@ -296,20 +301,23 @@ __device__ __forceinline__ uint32_t block_scan256(uint32_t x, uint32_t* s, uint3
 }
 
 // One chunk's staged segments -> compact payload: lane 8j + q moves units q, q+8, q+16 of
-// tile t0 + j (loads first, then stores).
+// tile t0 + j (loads first, then stores).  Converged call (the wave scan).
 __device__ __forceinline__ void copy_group(const uint64_t* __restrict__ stage, unsigned char* __restrict__ wire,
                                            const CodecGeom& g, int chunk, uint32_t base, int lane) {
     const int t = chunk * CODEC_TPW + (lane >> 3), q = lane & 7;
     const bool live = t < g.n_tiles;
-    const uint32_t meta = live ? wire_tile_hdr(wire)[2 * (size_t)t + 1] : 0u;
-    const uint32_t u = units_of(meta);
+    const uint32_t u = live ? units_of(widths_of_code(wire_tile_hdr(wire)[t] >> 24)) : 0u;
+    // offset inside the chunk: the units of the chunk's earlier tiles (wave scan, as the encoder)
+    const uint32_t u7 = q == 7 ? u : 0u;
+    const uint32_t incl = wave_scan_incl(u7);
+    const uint32_t rel = q == 7 ? incl - u7 : incl;
     uint64_t* pay = wire_payload(wire, g);
     uint64_t v[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) v[k] = q + 8 * k < (int)u ? stage[(size_t)t * STAGE_UNITS + q + 8 * k] : 0ull;
 #pragma unroll
     for (int k = 0; k < 3; ++k)
-        if (q + 8 * k < (int)u) pay[(size_t)base + (meta >> 12) + q + 8 * k] = v[k];
+        if (q + 8 * k < (int)u) pay[(size_t)base + rel + q + 8 * k] = v[k];
 }
 
 // Same workgroup ranges as encode_tiles_kernel: the base of workgroup b's chunks is the sum of
@@ -350,7 +358,7 @@ __global__ __launch_bounds__(256) void encode_copy_kernel(const uint64_t* __rest
         h[2] = (uint32_t)g.n_chunks;
         h[3] = (uint32_t)g.tiles_per_frame;
         if (wire_bytes) *wire_bytes = (int64_t)(g.fixed_bytes + 8 * (size_t)total);
-        const size_t used = 16 + 8 * (size_t)g.n_tiles + 4 * (size_t)g.n_chunks;
+        const size_t used = 16 + 4 * (size_t)g.n_tiles + 4 * (size_t)g.n_chunks;
         if (used < g.fixed_bytes) *(uint32_t*)(wire + used) = 0u;  // padding to 8 bytes
     }
 }
@@ -376,7 +384,7 @@ constexpr int DEC_TPW = CODEC_TPW;
 struct DecHead {
     const unsigned char* wire;
     int rank, t0;
-    uint2 hdr;      // this lane's tile: first pixel, meta
+    uint32_t hdr;   // this lane's tile: first pixel | width code << 24
     uint32_t base;  // the chunk's unit offset
 };
 __device__ __forceinline__ DecHead decode_head(const unsigned char* __restrict__ gathered, size_t rank_stride,
@@ -387,7 +395,7 @@ __device__ __forceinline__ DecHead decode_head(const unsigned char* __restrict__
     h.rank = g.rank + rel_rank;
     h.wire = gathered + (size_t)h.rank * rank_stride;
     const int t = h.t0 + (lane >> 3);
-    h.hdr = ((const uint2*)wire_tile_hdr(h.wire))[t < g.n_tiles ? t : 0];
+    h.hdr = wire_tile_hdr(h.wire)[t < g.n_tiles ? t : 0];
     h.base = wire_chunk_base(h.wire, g)[h.t0 / CODEC_TPW];  // the wave's chunk
     return h;
 }
@@ -401,45 +409,60 @@ __device__ __forceinline__ void decode_group(int32_t* __restrict__ frames, const
     const int j = lane >> 3, ry = lane & 7;
     const int t = t0 + j;
     const bool live = t < g.n_tiles;
-    const uint32_t first = live ? h.hdr.x : 0u, meta = live ? h.hdr.y : 0u;
-    const uint32_t base = h.base;
+    const uint32_t first = live ? h.hdr & 0xffffffu : 0u;
+    const uint32_t wm = live ? widths_of_code(h.hdr >> 24) : 0u;
+    const uint32_t u = units_of(wm);
+    // the tile's offset inside the chunk: the units of the chunk's earlier tiles (wave scan)
+    const uint32_t u7 = ry == 7 ? u : 0u;
+    const uint32_t incl = wave_scan_incl(u7);
+    const uint32_t rel = ry == 7 ? incl - u7 : incl;
     const TilePos tp = tile_pos(g, t0, j);
     const int f = tp.f, tr = tp.tr, tc = tp.tc;
     const int r = tr * 8 + ry;
     const int y = frame_row(g, rank, r);
     const bool row_ok = live && r < nb * g.band_rows && y < g.H;
     const int x0 = tc * 8;
-    // residual bytes of this row, channel by channel (width 0: nothing loaded, zeros)
-    const uint32_t w[3] = {meta & 15u, (meta >> 4) & 15u, (meta >> 8) & 15u};
     const uint64_t* pay = wire_payload(wire, g);
     uint32_t d[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) d[i] = 0u;
-    if (__builtin_amdgcn_ballot_w64((meta & 0xfffu) != 0) != 0) {  // some tile of the wave is not flat
-        uint32_t seg = base + (meta >> 12);  // unit offset of the channel's segment
+    if (__builtin_amdgcn_ballot_w64(u != 0) != 0) {  // some tile of the wave is not flat
+        uint32_t seg = h.base + rel;  // unit offset of the channel's segment
 #pragma unroll
         for (int c = 0; c < 3; ++c) {
-            const uint32_t wc = w[c];
-            const uint32_t byte = (uint32_t)ry * wc;  // row's first byte inside the segment
-            const uint64_t* src = wc ? pay + seg + (byte >> 3) : (const uint64_t*)wire;
-            const uint64_t bits = wc ? (*src >> (8 * (byte & 7))) : 0ull;
-            const uint32_t lo = (uint32_t)bits, hi = (uint32_t)(bits >> 32);
+            const uint32_t wc = (wm >> (4 * c)) & 15u;
+            uint64_t bits = 0;
+            if (wc) {  // this row's wc bytes [ry*wc, ry*wc + wc) of the segment: one or two loads
+                const uint32_t byte = (uint32_t)ry * wc, sb = byte & 7u;
+                const uint64_t* src = pay + seg + (byte >> 3);
+                const uint64_t lo = src[0];
+                const uint64_t hi = sb + wc > 8u ? src[1] : 0ull;  // (never past the segment)
+                bits = sb ? (lo >> (8 * sb)) | (hi << (64 - 8 * sb)) : lo;
+            }
             const uint32_t mask = (1u << wc) - 1u;
 #pragma unroll
-            for (int rx = 0; rx < 8; ++rx) {
-                const uint32_t pos = (uint32_t)rx * wc;
-                const uint32_t word = pos < 32 ? lo : hi;
-                d[rx] |= ((word >> (pos & 31)) & mask) << (16 - 8 * c);
-            }
+            for (int rx = 0; rx < 8; ++rx)
+                d[rx] |= ((uint32_t)(bits >> (rx * wc)) & mask) << (16 - 8 * c);
             seg += wc;
         }
 #pragma unroll
         for (int rx = 0; rx < 8; ++rx) d[rx] = unzigzag_bytes(d[rx]) & 0xffffffu;
+        // prefix over the tile's rows (lanes 8j..8j+7): Hillis-Steele, 3 row shifts
+#pragma unroll
+        for (int rx = 0; rx < 8; ++rx) {
+            uint32_t v = d[rx];
+            const uint32_t s1 = row_shr<1>(v);
+            v = ry >= 1 ? add_bytes(v, s1) : v;
+            const uint32_t s2 = row_shr<2>(v);
+            v = ry >= 2 ? add_bytes(v, s2) : v;
+            const uint32_t s4 = row_shr<4>(v);
+            v = ry >= 4 ? add_bytes(v, s4) : v;
+            d[rx] = v & 0xffffffu;
+        }
     }
-    // first column: pixel (0, ry) = first + d0(ry) (+ d0(ry - 1) in odd rows, from the lane above)
-    const uint32_t d0_above = row_shr<1>(d[0]);
+    // then along the row: column 0 holds p(0, ry) - first, columns >= 1 p(x) - p(x-1)
     uint32_t px[8];
-    px[0] = add_bytes(first, (ry & 1) ? add_bytes(d[0], d0_above) : d[0]) & 0xffffffu;
+    px[0] = add_bytes(first, d[0]) & 0xffffffu;
 #pragma unroll
     for (int rx = 1; rx < 8; ++rx) px[rx] = add_bytes(px[rx - 1], d[rx]) & 0xffffffu;
     // A group of 8 tiles of one tile row, inside the width, on 16-byte aligned rows (wave-uniform;

@@ -14,7 +14,7 @@ PKG_ROOT = os.path.dirname(_HERE)
 # RAYTRACER_HIP_LIB selects another build of the library (A/B variants under lib/ab/)
 LIB_PATH = os.environ.get("RAYTRACER_HIP_LIB") or os.path.join(PKG_ROOT, "lib", "libraytracer_hip.so")
 
-RT_ABI_VERSION = 5  # include/raytracer_hip.h
+RT_ABI_VERSION = 6  # include/raytracer_hip.h
 RT_CREATE_RCCL_GATHER = 1
 RT_BANDS_INT32, RT_BANDS_RGB24, RT_BANDS_FRAME = 0, 1, 2
 RT_OK = 0
