@@ -332,10 +332,14 @@ constexpr unsigned CNT_REFL_MASK = 0xFFu;
 // SURVEY.md 8(d), which count every primitive of every ray.
 // SMAX > 0: the scene has at most SMAX spheres (a compile-time bound: the pair loops over the
 // sphere table are unrolled, no loop counter or pointer arithmetic on the scalar unit).
+#ifndef RT_SLOT_TALLY
+#define RT_SLOT_TALLY 0
+#endif
 template <bool ON, int SMAX = 0>
 struct Tally {
     static constexpr int smax = SMAX;
     __device__ __forceinline__ void sphere(bool) {}
+    __device__ __forceinline__ void shadow_sphere(bool) {}
     __device__ __forceinline__ void plane(bool) {}
     __device__ __forceinline__ void shadow(bool) {}
 };
@@ -343,7 +347,10 @@ template <int SMAX>
 struct Tally<true, SMAX> {
     static constexpr int smax = SMAX;
     unsigned s = 0, pl = 0, sh = 0;
-    __device__ __forceinline__ void sphere(bool c) { s += c ? 1u : 0u; }
+    // RT_SLOT_TALLY (diagnostic builds, tools/slot_probe.py): lane slots of the exact tests,
+    // useful or not -- 1: every sphere test, 2: the nearest-hit tests only
+    __device__ __forceinline__ void sphere(bool c) { s += (RT_SLOT_TALLY || c) ? 1u : 0u; }
+    __device__ __forceinline__ void shadow_sphere(bool c) { s += (RT_SLOT_TALLY == 1 || c) ? 1u : 0u; }
     __device__ __forceinline__ void plane(bool c) { pl += c ? 1u : 0u; }
     __device__ __forceinline__ void shadow(bool c) { sh += c ? 1u : 0u; }
 };
@@ -445,9 +452,9 @@ __device__ __forceinline__ bool shadow_scan(const LaunchParams& p, f3 hp, const 
     int blk = 0;
     for_sphere_pairs<T>(p, [&](int i) {
         const DevSphere s0 = p.sph[i], s1 = p.sph[i + 1];
-        tl.sphere(blk == 0);
+        tl.shadow_sphere(blk == 0);
         blk = shadow_blocked<A2OK>(hp, l, false, s0) ? 1 : blk;
-        tl.sphere((blk == 0) & (i + 1 < p.S));
+        tl.shadow_sphere((blk == 0) & (i + 1 < p.S));
         blk = shadow_blocked<A2OK>(hp, l, false, s1) ? 1 : blk;
     });
     return blk != 0;
@@ -1071,9 +1078,9 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
                         const int i1 = two ? base + (int)__builtin_ctzll(mk64) : i0;
                         if (two) mk64 &= mk64 - 1;
                         const DevSphere s0 = p.sph[i0], s1 = p.sph[i1];
-                        tl.sphere(!blocked);
+                        tl.shadow_sphere(!blocked);
                         const bool h0 = shadow_blocked<false, true>(hs, l, l_ok, s0);
-                        tl.sphere(two && !blocked && !h0);
+                        tl.shadow_sphere(two && !blocked && !h0);
                         const bool h1 = shadow_blocked<false, true>(hs, l, l_ok, s1);
                         blocked = blocked | h0 | h1;  // no short-circuit branch
                         if (__builtin_amdgcn_ballot_w64(!blocked) == 0) break;
