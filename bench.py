@@ -359,10 +359,6 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=world)
     else:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
-    if args.band_format == "tiles" and not args.no_pipeline and args.inflight > 2:
-        # the next-but-one batch reuses raw[b % 2]: with a third trace stream it could overwrite the
-        # band set that encode(b) still reads
-        raise SystemExit("bench.py: the tile pipeline supports --inflight 1 or 2")
     sc = scenes.config(args.config)
     if args.size:
         w_, h_ = map(int, args.size.lower().split("x"))
@@ -439,8 +435,8 @@ def main():
                 # one launch per batch (F frames of this rank's bands, each in full; a rank's share
                 # of a 1080p frame is too little GPU work for a launch per frame), batches
                 # alternating between the trace streams; at a batch end the encode runs on
-                # `stream` after the batch's stream joined it, and that trace stream waits for it
-                # (the next-but-one batch reuses the raw buffer)
+                # `stream` after the batch's stream joined it, and every trace stream waits for it
+                # (the next-but-one batch reuses the raw buffer, on any of them at --inflight >= 3)
                 done = 0
                 while done < n:
                     m = min(tg.F - tg.k % tg.F, n - done)
@@ -455,8 +451,9 @@ def main():
                         stream.wait_stream(ts)
                     for _ in range(m):
                         tg.commit(stream)
-                    if end and ts is not stream:
-                        ts.wait_stream(stream)
+                    if end:
+                        for t in tstreams[1:]:
+                            t.wait_stream(stream)
                     done += m
 
             def finish():  # noqa: F811  -- the last (possibly partial) batch, every stage
@@ -465,6 +462,8 @@ def main():
                 tg.drain(stream)
                 stream.wait_stream(tg.comm)
                 stream.wait_stream(tg.dec)
+                for t in tstreams[1:]:  # (the next run's batches reuse the raw buffers)
+                    t.wait_stream(stream)
         else:
             fmt = abi.RT_BANDS_RGB24 if args.band_format == "rgb24" else abi.RT_BANDS_INT32
             bgb = BatchedBandGather(rb, torch.device("cuda", local), frames_per_batch=args.batch,

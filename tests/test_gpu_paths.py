@@ -138,6 +138,7 @@ def _free_port():
 
 
 @pytest.mark.parametrize("extra,shape", [(["--rank0-codec"], "small"), ([], "small"),
+                                         (["--rank0-codec", "--inflight", "3"], "small"),
                                          (["--rank0-codec"], "full"), (["--rank0-codec"], "short")])
 def test_tile_pipeline_on_cuda_streams(extra, shape):
     """bench.py's N>1 tile pipeline (encode, size all_reduce, gather, decode on side streams,
@@ -145,7 +146,9 @@ def test_tile_pipeline_on_cuda_streams(extra, shape):
     frame left in its rings against a single-launch render (--verify, exit 3 on a mismatch).
     "full": 1080p C2, 300 frames in batches of 64 with speculative gather sizes -- the shape that
     exposed speculative gathers not ordered after their encode (fixed by an encode event);
-    "short": the driver's 20 frames, one batch through the gather-first path."""
+    "short": the driver's 20 frames, one batch through the gather-first path.  --inflight 3:
+    batches on three trace streams (every one waits for the encode of the batch whose raw buffer
+    it reuses)."""
     env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
     env.pop("WORLD_SIZE", None)
     size = {"small": ["--size", "640x360", "--steps", "40", "--warmup", "16", "--batch", "8"],
