@@ -79,6 +79,10 @@ def parse(argv=None):
     ap.add_argument("--rank0-codec", action="store_true",
                     help="N>1 tiles: rank 0 encodes and decodes its own bands too (instead of rendering them "
                          "straight into its frames); the one-process rehearsal uses it to exercise the codec")
+    ap.add_argument("--no-fuse", action="store_true",
+                    help="N>1 tiles: trace into an int32 band set and encode it (rt_encode_bands) instead of "
+                         "tracing straight into the wire (rt_render_bands_tiles + rt_finish_wire: the encoder fused "
+                         "into the trace kernel's epilogue, the band set never written)")
     ap.add_argument("--no-speculate", action="store_true",
                     help="N>1 tiles: read every batch's reduced wire size back before its gather (default: after "
                          "the warm-up, gather at 1.25 x the largest wire per frame seen so far right behind the size "
@@ -407,9 +411,12 @@ def main():
             from raytracer_hip.dist import TileBandGather
 
             def t_encode(raw, n, wire, size, st):
-                ctx.encode_bands(W, H, rb.band_rows, band_rank, band_world, raw.data_ptr(), rb.slot_elems, n,
-                                 wire.data_ptr(),
-                                 size.data_ptr(), st.cuda_stream)
+                if raw is None:  # fused: the batch was traced into the wire; finish it
+                    ctx.finish_wire(W, H, rb.band_rows, band_rank, band_world, n, wire.data_ptr(), size.data_ptr(),
+                                    st.cuda_stream)
+                else:
+                    ctx.encode_bands(W, H, rb.band_rows, band_rank, band_world, raw.data_ptr(), rb.slot_elems, n,
+                                     wire.data_ptr(), size.data_ptr(), st.cuda_stream)
 
             def t_decode(recv, rank_stride, n, frames_, st, first_rank):
                 ctx.decode_gathered(W, H, rb.band_rows, band_world, recv.data_ptr(), rank_stride, n, frames_.data_ptr(),
@@ -417,7 +424,8 @@ def main():
 
             tg = TileBandGather(rb, torch.device("cuda", local), args.batch,
                                 lambda n: wire_layout(W, H, rb.band_rows, band_world, n), t_encode, t_decode,
-                                rank0_codec=args.rank0_codec, compositor=comp, phys_rank=rank, phys_world=world)
+                                rank0_codec=args.rank0_codec, compositor=comp, phys_rank=rank, phys_world=world,
+                                fused=not args.no_fuse)
             out_fmt = abi.RT_BANDS_FRAME if tg.direct else abi.RT_BANDS_INT32
             # frames alternate between trace streams (two in flight per rank); at a batch end the
             # encode runs on `stream` after the others joined it, and the trace streams then wait
@@ -443,7 +451,10 @@ def main():
                     ts = tstreams[(tg.k // tg.F) % len(tstreams)]
                     if tg.k % tg.F == 0:
                         tg.begin_batch([ts])
-                    if not tg.idle:  # (the compositor rank only assembles)
+                    if tg.fused:  # straight into the batch's wire (tile headers + codec scratch)
+                        ctx.render_bands_tiles(W, H, rb.band_rows, band_rank, band_world, tg.k % tg.F, m, tg.F,
+                                               tg.wire_target().data_ptr(), ts.cuda_stream)
+                    elif not tg.idle:  # (the compositor rank only assembles)
                         ctx.render_bands_batch(W, H, rb.band_rows, band_rank, band_world, m, tg.target().data_ptr(),
                                                stride_b, out_fmt, ts.cuda_stream)
                     end = (tg.k + m) % tg.F == 0
@@ -516,7 +527,7 @@ def main():
     # no event pairs around the launches of the timed region (each pair costs ~9 us of GPU time,
     # tools/region_probe.py): the kernel duration comes from an untimed second pass (below)
     ctx.set_timing(0)
-    if tg is not None and not tg.idle and not tg.direct:
+    if tg is not None and not tg.idle and not tg.direct and not tg.fused:
         # size the codec's scratch for a whole batch before anything is timed (rt_encode_bands grows
         # it on demand, behind a device synchronisation)
         t_encode(tg.raw[0], tg.F, tg.wire[0], tg.size[0], stream)

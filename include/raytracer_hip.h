@@ -269,6 +269,16 @@ int rt_encode_bands(rt_ctx* ctx, int width, int height, int band_rows, int rank,
 int rt_decode_gathered(rt_ctx* ctx, int width, int height, int band_rows, int world, int first_rank,
                        const void* d_gathered, size_t rank_stride, int n_frames, int32_t* d_frames,
                        size_t frame_stride, void* hip_stream);
+/* The encoder fused into the trace (ABI 6): trace frames frame0 .. frame0+n_frames-1 of a batch
+ * of batch_frames of `rank`'s bands straight into d_wire's tile headers and the context's codec
+ * scratch -- the band set never reaches HBM -- then rt_finish_wire turns the batch's first
+ * n_frames (<= batch_frames) into the same wire rt_encode_bands would have made of the band sets
+ * (byte for byte).  A batch may take several rt_render_bands_tiles calls; the context's scratch
+ * holds one batch at a time (stream-ordered, like rt_encode_bands').  Asynchronous on hip_stream. */
+int rt_render_bands_tiles(rt_ctx* ctx, int width, int height, int band_rows, int rank, int world,
+                          int frame0, int n_frames, int batch_frames, void* d_wire, void* hip_stream);
+int rt_finish_wire(rt_ctx* ctx, int width, int height, int band_rows, int rank, int world, int n_frames,
+                   void* d_wire, int64_t* d_wire_bytes, void* hip_stream);
 
 /* ---- double-buffered frames ------------------------------ */
 /* Asynchronous Tick(): captures the current camera, enqueues the trace and the D2H copy

@@ -108,6 +108,54 @@ def test_traced_band_sets_roundtrip_to_the_frame(gpu_ctx, cfg, world, band_rows,
     assert total < 3 * W * H  # smaller than the RGB24 band sets
 
 
+@pytest.mark.parametrize("cfg,size,world,band_rows,F,splits", [
+    ("C2", (1920, 1080), 2, 8, 2, (2,)), ("C3", (640, 360), 3, 8, 4, (1, 2)), ("C4", (320, 180), 4, 8, 2, (2,)),
+    ("REF", (203, 97), 3, 5, 3, (3,)), ("C2", (131, 67), 1, 8, 4, (1, 1, 2)), ("C4", (96, 54), 8, 4, 2, (1, 1))])
+def test_fused_encoder_wire_equals_host_mirror(gpu_ctx, cfg, size, world, band_rows, F, splits):
+    """rt_render_bands_tiles (the encoder fused into the trace kernels' epilogue, the band set never
+    written) + rt_finish_wire give every rank the same bytes as the host mirror's encoding of the
+    rank's traced band set -- direct and bundle kernels, ragged frames, band heights other than 8,
+    ranks with fewer bands (their untraced tile rows), a batch traced in several launches and a
+    finish over fewer frames than the batch holds.  The scratch and wire start dirty."""
+    import torch
+    from raytracer_hip import abi
+    sc = scenes.config(cfg).resized(*size)
+    W, H = size
+    gpu_ctx.set_scene(sc)
+    s = torch.cuda.current_stream().cuda_stream
+    lay = tc.layout(W, H, band_rows, world, F)
+    n = sum(splits)  # frames traced (<= F)
+    for r in range(world):
+        rb = RowBands(W, H, band_rows, r, world)
+        buf = torch.zeros(rb.slot_elems, dtype=torch.int32, device="cuda")
+        gpu_ctx.render_bands_ex(W, H, band_rows, r, world, buf.data_ptr(), abi.RT_BANDS_INT32, s)
+        torch.cuda.synchronize()
+        bs = np.tile(buf.cpu().numpy(), n)  # every frame of the batch has the same camera
+        want = tc.encode(bs, W, H, band_rows, r, world, n)
+        wire = torch.full((lay.max_bytes + 8,), 0xA5, dtype=torch.uint8, device="cuda")
+        size_t = torch.zeros(1, dtype=torch.int64, device="cuda")
+        f0 = 0
+        for m in splits:
+            gpu_ctx.render_bands_tiles(W, H, band_rows, r, world, f0, m, F, wire.data_ptr(), s)
+            f0 += m
+        gpu_ctx.finish_wire(W, H, band_rows, r, world, n, wire.data_ptr(), size_t.data_ptr(), s)
+        torch.cuda.synchronize()
+        assert int(size_t.item()) == len(want), (r, int(size_t.item()), len(want))
+        assert wire[:len(want)].cpu().numpy().tobytes() == want, f"rank {r}: fused wire differs from the host mirror"
+
+
+def test_fused_encoder_rejects_bad_arguments(gpu_ctx):
+    import torch
+    from raytracer_hip import RayTracerError
+    wire = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
+    with pytest.raises(RayTracerError):  # frames past the batch
+        gpu_ctx.render_bands_tiles(64, 64, 8, 0, 1, 1, 2, 2, wire.data_ptr())
+    with pytest.raises(RayTracerError):  # rank out of range
+        gpu_ctx.render_bands_tiles(64, 64, 8, 2, 2, 0, 1, 1, wire.data_ptr())
+    with pytest.raises(RayTracerError):  # misaligned wire
+        gpu_ctx.render_bands_tiles(64, 64, 8, 0, 1, 0, 1, 1, wire.data_ptr() + 4)
+
+
 def test_encode_rejects_bad_arguments(gpu_ctx):
     import torch
     from raytracer_hip import RayTracerError

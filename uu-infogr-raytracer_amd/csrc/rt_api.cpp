@@ -410,9 +410,17 @@ int view_tables(rt_ctx* ctx, Device& d, LaunchParams& lp) {
     return RT_OK;
 }
 
+// The fused encoder's target of a trace with out_fmt OUT_TILES (rt_render_bands_tiles).
+struct EncTarget {
+    unsigned char* wire;
+    uint32_t* stage;
+    int tiles_x, tpf, frame0;
+};
+
 // Launch the trace of bands (first, step) of `band_rows` rows into `out` on device d.
 int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int band_rows, int first, int step,
-                int32_t* out, int* n_bands, int fmt = RT_BANDS_INT32, int n_frames = 1, size_t frame_bytes = 0) {
+                int32_t* out, int* n_bands, int fmt = RT_BANDS_INT32, int n_frames = 1, size_t frame_bytes = 0,
+                const EncTarget* enc = nullptr) {
     LaunchParams lp;
     std::memset(&lp, 0, sizeof lp);
     int rc = view_params(ctx, W, H, lp);
@@ -428,6 +436,11 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
     lp.out_fmt = fmt;
     lp.n_frames = n_frames;
     lp.out_frame_bytes = frame_bytes;
+    if (enc) {
+        lp.out_fmt = OUT_TILES;
+        lp.enc_wire = enc->wire, lp.enc_stage = enc->stage;
+        lp.enc_tiles_x = enc->tiles_x, lp.enc_tpf = enc->tpf, lp.enc_frame0 = enc->frame0;
+    }
     hipStream_t saved = d.stream;
     d.stream = stream;
     const bool timed = begin_timed(ctx, d, 0);
@@ -862,6 +875,20 @@ static bool codec_geom(int width, int height, int band_rows, int world, int n_fr
     return true;
 }
 
+// Codec scratch of device d for geometry g (staged segments + workgroup sums), grown on demand:
+// the previous user of the old buffer may still run, so growing waits for the device first.
+static int ensure_stage(rt_ctx* ctx, Device& d, const rtk::CodecGeom& g) {
+    const size_t need = encode_stage_bytes(g);
+    if (need > d.stage_cap) {
+        HIP_TRY(ctx, hipDeviceSynchronize());
+        if (d.d_stage) HIP_TRY(ctx, hipFree(d.d_stage));
+        d.d_stage = nullptr, d.stage_cap = 0;
+        HIP_TRY(ctx, hipMalloc(&d.d_stage, need));
+        d.stage_cap = need;
+    }
+    return RT_OK;
+}
+
 int rt_wire_layout_of(int width, int height, int band_rows, int world, int n_frames, rt_wire_layout* out) {
     rtk::CodecGeom g;
     if (!out || !codec_geom(width, height, band_rows, world, n_frames, g, out))
@@ -882,18 +909,49 @@ int rt_encode_bands(rt_ctx* ctx, int width, int height, int band_rows, int rank,
     g.frame_stride = frame_stride;
     Device& d = ctx->dev[0];
     DeviceGuard guard(d.id);
-    // codec scratch (staged segments + workgroup sums), grown on demand: the previous user of the
-    // old buffer may still run, so growing waits for the device first
-    const size_t need = encode_stage_bytes(g);
-    if (need > d.stage_cap) {
-        HIP_TRY(ctx, hipDeviceSynchronize());
-        if (d.d_stage) HIP_TRY(ctx, hipFree(d.d_stage));
-        d.d_stage = nullptr, d.stage_cap = 0;
-        HIP_TRY(ctx, hipMalloc(&d.d_stage, need));
-        d.stage_cap = need;
-    }
+    const int rc = ensure_stage(ctx, d, g);
+    if (rc != RT_OK) return rc;
     int e = launch_encode_bands(d_bands, (unsigned char*)d_wire, g, d_wire_bytes, d.d_stage, hip_stream);
     if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "encode launch: %s", hipGetErrorString((hipError_t)e));
+    return RT_OK;
+}
+
+int rt_render_bands_tiles(rt_ctx* ctx, int width, int height, int band_rows, int rank, int world, int frame0,
+                          int n_frames, int batch_frames, void* d_wire, void* hip_stream) {
+    int rc = check_ctx(ctx, width, height);
+    if (rc != RT_OK) return rc;
+    rtk::CodecGeom g;
+    if (!codec_geom(width, height, band_rows, world, batch_frames, g, nullptr) || rank < 0 || rank >= world ||
+        frame0 < 0 || n_frames <= 0 || n_frames > 65535 || frame0 + n_frames > batch_frames || !d_wire ||
+        ((uintptr_t)d_wire & 7) != 0)
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_bands_tiles: bad arguments");
+    if (ctx->n_gpus != 1) return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_bands_tiles needs a single-GPU context");
+    Device& d = ctx->dev[0];
+    DeviceGuard guard(d.id);
+    rc = ensure_stage(ctx, d, g);
+    if (rc != RT_OK) return rc;
+    const EncTarget enc{(unsigned char*)d_wire, (uint32_t*)d.d_stage, g.tiles_x, g.tiles_per_frame, frame0};
+    int nb = 0;
+    rc = trace_bands(ctx, d, (hipStream_t)hip_stream, width, height, band_rows, rank, world, (int32_t*)d_wire, &nb,
+                     RT_BANDS_INT32, n_frames, 0, &enc);
+    if (rc == RT_OK) ctx->pixels += (uint64_t)nb * band_rows * width * (uint64_t)n_frames;
+    return rc;
+}
+
+int rt_finish_wire(rt_ctx* ctx, int width, int height, int band_rows, int rank, int world, int n_frames,
+                   void* d_wire, int64_t* d_wire_bytes, void* hip_stream) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "NULL context");
+    rtk::CodecGeom g;
+    if (!codec_geom(width, height, band_rows, world, n_frames, g, nullptr) || rank < 0 || rank >= world ||
+        !d_wire || ((uintptr_t)d_wire & 7) != 0)
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_finish_wire: bad arguments");
+    Device& d = ctx->dev[0];
+    DeviceGuard guard(d.id);
+    if (!d.d_stage || encode_stage_bytes(g) > d.stage_cap)
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_finish_wire: no rt_render_bands_tiles batch of %d frames", n_frames);
+    const int traced_rows = (bands_of(height, band_rows, rank, world) * band_rows + 7) / 8;
+    int e = launch_finish_wire((unsigned char*)d_wire, g, traced_rows, d_wire_bytes, d.d_stage, hip_stream);
+    if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "finish launch: %s", hipGetErrorString((hipError_t)e));
     return RT_OK;
 }
 

@@ -28,24 +28,20 @@
 #include <algorithm>
 #include <cstdint>
 
+#include "rt_codec_common.h"
 #include "rt_internal.h"
 
 namespace rtk {
 
-constexpr int CODEC_TPW = 8;     // tiles per wave = tiles per chunk
 #ifndef RT_ENC_BLOCKS
 #define RT_ENC_BLOCKS 2048
 #endif
 constexpr int CODEC_BLOCKS = RT_ENC_BLOCKS;  // encode grid: 256 CUs x 8 workgroups of 4 waves
 constexpr int CODEC_MAX_PER = 1024;  // chunks per workgroup at most (LDS of the copy pass)
-constexpr int STAGE_WORDS = 48;  // staging words per tile (3 channels x 8 bits x 64 lanes / 32)
-constexpr int STAGE_UNITS = STAGE_WORDS / 2;
 
 // Wave index inside the workgroup, as a scalar: what derives from it stays wave-uniform.
 __device__ __forceinline__ int wave_index() { return __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6)); }
 
-__device__ __forceinline__ const uint32_t* wire_tile_hdr(const unsigned char* w) { return (const uint32_t*)(w + 16); }
-__device__ __forceinline__ uint32_t* wire_tile_hdr(unsigned char* w) { return (uint32_t*)(w + 16); }
 __device__ __forceinline__ uint32_t* wire_chunk_base(unsigned char* w, const CodecGeom& g) {
     return (uint32_t*)(w + 16 + 4 * (size_t)g.n_tiles);
 }
@@ -59,29 +55,6 @@ __device__ __forceinline__ const uint64_t* wire_payload(const unsigned char* w, 
     return (const uint64_t*)(w + g.fixed_bytes);
 }
 
-// Byte-wise (mod 256 per byte) add / subtract of packed 0x00RRGGBB values.
-__device__ __forceinline__ uint32_t add_bytes(uint32_t a, uint32_t b) {
-    return ((a & 0x7f7f7f7fu) + (b & 0x7f7f7f7fu)) ^ ((a ^ b) & 0x80808080u);
-}
-__device__ __forceinline__ uint32_t sub_bytes(uint32_t a, uint32_t b) {
-    return ((a | 0x80808080u) - (b & 0x7f7f7f7fu)) ^ ((a ^ ~b) & 0x80808080u);
-}
-// zigzag of each byte read as int8: 0, -1, 1, -2, ... -> 0, 1, 2, 3, ...
-__device__ __forceinline__ uint32_t zigzag_bytes(uint32_t d) {
-    const uint32_t neg = (d >> 7) & 0x01010101u;      // sign bit of each byte
-    return ((d << 1) & 0xfefefefeu) ^ (neg * 0xffu);  // (s << 1) ^ (s >> 7) per byte
-}
-__device__ __forceinline__ uint32_t unzigzag_bytes(uint32_t z) {
-    const uint32_t odd = z & 0x01010101u;
-    return ((z >> 1) & 0x7f7f7f7fu) ^ (odd * 0xffu);  // (z >> 1) ^ -(z & 1) per byte
-}
-
-// DPP row shift right by N lanes inside each 16-lane row (0 shifted in).
-template <int N>
-__device__ __forceinline__ uint32_t row_shr(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x110 + N, 0xf, 0xf, true);
-}
-
 // RT_ENC_DPP: the encoder's cross-lane steps without LDS round trips (ds_bpermute): the tile's
 // first pixel by a quad broadcast + a 4-lane shift into the upper quad, the tile OR as an
 // all-lanes butterfly (quad xor 1, quad xor 2, half-row mirror), the chunk-relative offsets
@@ -89,45 +62,6 @@ __device__ __forceinline__ uint32_t row_shr(uint32_t v) {
 #ifndef RT_ENC_DPP
 #define RT_ENC_DPP 1
 #endif
-template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf, bool BOUND = true>
-__device__ __forceinline__ uint32_t dpp(uint32_t old, uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, CTRL, ROW_MASK, BANK_MASK, BOUND);
-}
-// lane 8j's value in every lane of its 8-lane group
-__device__ __forceinline__ uint32_t group8_first(uint32_t v) {
-    const uint32_t q = dpp<0x00>(0u, v);            // quad_perm [0,0,0,0]
-    return dpp<0x114, 0xf, 0xa, false>(q, q);        // row_shr:4 into lanes 4-7, 12-15 of each row
-}
-// OR of the 8 lanes of each group, in every lane
-__device__ __forceinline__ uint32_t group8_or(uint32_t v) {
-    v |= dpp<0xb1>(0u, v);   // quad_perm [1,0,3,2]
-    v |= dpp<0x4e>(0u, v);   // quad_perm [2,3,0,1]
-    v |= dpp<0x141>(0u, v);  // row_half_mirror
-    return v;
-}
-// inclusive scan over the wave (all 64 lanes active)
-__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
-    x += row_shr<1>(x);
-    x += row_shr<2>(x);
-    x += row_shr<4>(x);
-    x += row_shr<8>(x);
-    x += dpp<0x142, 0xa, 0xf, false>(0u, x);  // row_bcast:15 -> rows 1, 3
-    x += dpp<0x143, 0xc, 0xf, false>(0u, x);  // row_bcast:31 -> rows 2, 3
-    return x;
-}
-
-__device__ __forceinline__ uint32_t units_of(uint32_t wm) { return (wm & 15u) + ((wm >> 4) & 15u) + ((wm >> 8) & 15u); }
-// Widths WIDTHS = {0, 2, 3, 4, 6, 8} by index (nibbles of 0x864320); a tile's width code is
-// i_R + 6 i_G + 36 i_B (< 216, the header's top byte).
-__device__ __forceinline__ uint32_t width_at(uint32_t i) { return (0x864320u >> (4u * i)) & 15u; }
-// widths of a code as wm = w_R | w_G << 4 | w_B << 8
-__device__ __forceinline__ uint32_t widths_of_code(uint32_t code) {
-    return width_at(code % 6u) | (width_at(code / 6u % 6u) << 4) | (width_at(code / 36u) << 8);
-}
-// Width index of a channel: bit length of its OR of zigzag residuals rounded up to a width.
-__device__ __forceinline__ uint32_t width_index(uint32_t o) {
-    return o == 0 ? 0u : o < 4 ? 1u : o < 8 ? 2u : o < 16 ? 3u : o < 64 ? 4u : 5u;
-}
 
 // Local row r of band set `rank` -> frame row.
 __device__ __forceinline__ int frame_row(const CodecGeom& g, int rank, int r) {
@@ -242,22 +176,7 @@ __device__ __forceinline__ uint32_t encode_group(unsigned char* __restrict__ wir
             uint64_t acc = 0;
 #pragma unroll
             for (int rx = 0; rx < 8; ++rx) acc |= (uint64_t)((z[rx] >> sh) & 0xffu) << (rx * w);
-            unsigned char* dst = seg + ry * w;
-            if (w == 8) {
-                *(uint64_t*)dst = acc;
-            } else if (w == 4) {
-                *(uint32_t*)dst = (uint32_t)acc;
-            } else if (w == 2) {
-                *(uint16_t*)dst = (uint16_t)acc;
-            } else if (w == 6) {  // 6 ry: 2-byte aligned
-                ((uint16_t*)dst)[0] = (uint16_t)acc;
-                ((uint16_t*)dst)[1] = (uint16_t)(acc >> 16);
-                ((uint16_t*)dst)[2] = (uint16_t)(acc >> 32);
-            } else if (w == 3) {
-                dst[0] = (unsigned char)acc;
-                dst[1] = (unsigned char)(acc >> 8);
-                dst[2] = (unsigned char)(acc >> 16);
-            }
+            store_row_bits(seg + ry * w, w, acc);
             seg += 8 * w;
         }
     }
@@ -277,6 +196,35 @@ __global__ __launch_bounds__(256) void encode_tiles_kernel(const int32_t* __rest
     uint32_t mine = 0;
     for (int chunk = lo + wave; chunk < hi; chunk += 4)
         mine += encode_group(wire, stage, g, chunk, lane, encode_load(bands, g, chunk, lane));
+    if (lane == 0) s_tot[wave] = mine;
+    __syncthreads();
+    if (threadIdx.x == 0) wg_total[blockIdx.x] = s_tot[0] + s_tot[1] + s_tot[2] + s_tot[3];
+}
+
+// After traces with OUT_TILES (the encoder fused into rt_kernel.hip): the chunk totals from the
+// tile headers alone (the encode_tiles_kernel ranges and outputs, no band-set read).  Tile rows
+// >= traced_rows of a frame were not traced: their headers are zeroed here.
+__global__ __launch_bounds__(256) void chunk_totals_kernel(unsigned char* __restrict__ wire,
+                                                          uint32_t* __restrict__ wg_total, CodecGeom g, int per,
+                                                          int traced_rows) {
+    __shared__ uint32_t s_tot[4];
+    const int lane = threadIdx.x & 63, wave = wave_index();
+    const int j = lane >> 3, ry = lane & 7;
+    const int lo = blockIdx.x * per, hi = min(g.n_chunks, lo + per);
+    uint32_t mine = 0;
+    for (int chunk = lo + wave; chunk < hi; chunk += 4) {
+        const int t = chunk * CODEC_TPW + j;
+        uint32_t hdr = 0;
+        if (t < g.n_tiles) {
+            uint32_t* h = wire_tile_hdr(wire) + t;
+            if ((t % g.tiles_per_frame) / g.tiles_x < traced_rows) hdr = *h;
+            else if (ry == 0) *h = 0u;
+        }
+        const uint32_t u7 = ry == 7 ? units_of(widths_of_code(hdr >> 24)) : 0u;
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)wave_scan_incl(u7), 63);
+        if (lane == 63) wire_chunk_base(wire, g)[chunk] = total;
+        mine += total;
+    }
     if (lane == 0) s_tot[wave] = mine;
     __syncthreads();
     if (threadIdx.x == 0) wg_total[blockIdx.x] = s_tot[0] + s_tot[1] + s_tot[2] + s_tot[3];
@@ -545,6 +493,22 @@ int launch_encode_bands(const int32_t* bands, unsigned char* wire, const CodecGe
     uint32_t* st = (uint32_t*)stage;
     uint32_t* wg_total = st + (size_t)g.n_chunks * CODEC_TPW * STAGE_WORDS;
     hipLaunchKernelGGL(encode_tiles_kernel, dim3((unsigned)blocks), dim3(256), 0, s, bands, wire, st, wg_total, g, per);
+    hipLaunchKernelGGL(encode_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const uint64_t*)st, wire,
+                       (const uint32_t*)wg_total, g, per, wire_bytes);
+    return (int)hipGetLastError();
+}
+
+int launch_finish_wire(unsigned char* wire, const CodecGeom& g, int traced_tile_rows, int64_t* wire_bytes,
+                       void* stage, void* stream) {
+    hipStream_t s = (hipStream_t)stream;
+    long long blocks = std::min<long long>((g.n_chunks + 3) / 4, CODEC_BLOCKS);  // as launch_encode_bands
+    int per = (int)((g.n_chunks + blocks - 1) / blocks);
+    if (per > CODEC_MAX_PER) per = CODEC_MAX_PER;
+    blocks = (g.n_chunks + per - 1) / per;
+    uint32_t* st = (uint32_t*)stage;
+    uint32_t* wg_total = st + (size_t)g.n_chunks * CODEC_TPW * STAGE_WORDS;
+    hipLaunchKernelGGL(chunk_totals_kernel, dim3((unsigned)blocks), dim3(256), 0, s, wire, wg_total, g, per,
+                       traced_tile_rows);
     hipLaunchKernelGGL(encode_copy_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const uint64_t*)st, wire,
                        (const uint32_t*)wg_total, g, per, wire_bytes);
     return (int)hipGetLastError();

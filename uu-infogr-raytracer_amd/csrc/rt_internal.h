@@ -123,7 +123,13 @@ struct LaunchParams {
     int n_frames;  // grid z (frames of one batch launch, all with this view); 0 = 1
     int32_t* out;
     unsigned long long out_frame_bytes;  // batch launches: frame z of the grid at (char*)out + z * out_frame_bytes
-    int out_fmt;  // 0: int32 0x00RRGGBB per pixel; 1: packed 24-bit (bytes B, G, R); 2: int32 at frame row y
+    int out_fmt;  // 0: int32 0x00RRGGBB per pixel; 1: packed 24-bit (bytes B, G, R); 2: int32 at frame row y;
+                  // 3 (OUT_TILES): the tile codec's encoder fused into the trace -- nothing at `out`,
+                  // tile t's header into enc_wire and its segments into enc_stage[t * STAGE_WORDS],
+                  // t = (enc_frame0 + frame) * enc_tpf + tile row * enc_tiles_x + tile column
+    unsigned char* enc_wire;
+    uint32_t* enc_stage;
+    int enc_tiles_x, enc_tpf, enc_frame0;
     unsigned long long* counters;  // COUNTER_SLOTS x COUNTER_STRIDE (CNT_*)
     int prim_const;                // 1: pc[0..S) and pbox[0..S) valid (S <= MAX_PRIM_CONST)
     PrimConst pc[MAX_PRIM_CONST];
@@ -148,6 +154,8 @@ int launch_scatter_gathered(const unsigned char* g, size_t slot_bytes, int fmt, 
 int launch_scatter_bands(const int32_t* bands, int32_t* frame, int W, int H, int band_rows, int band_first,
                          int band_step, int n_bands, void* stream);
 
+constexpr int OUT_TILES = 3;
+
 // Band-set tile codec (rt_codec.hip; format: raytracer_hip/tilecodec.py).
 struct CodecGeom {
     int W, H, band_rows, rank, world, n_bands;  // rank / n_bands: the encoder's rank; the decoder's first rank
@@ -161,6 +169,11 @@ struct CodecGeom {
 int launch_encode_bands(const int32_t* bands, unsigned char* wire, const CodecGeom& g, int64_t* wire_bytes,
                         void* stage, void* stream);
 size_t encode_stage_bytes(const CodecGeom& g);
+// The second half of the encoder after traces with OUT_TILES filled the tile headers (tile rows
+// >= traced_tile_rows of every frame were not traced: their headers are zeroed) and the staging
+// slots: chunk totals from the headers, then the compaction of launch_encode_bands.  Two launches.
+int launch_finish_wire(unsigned char* wire, const CodecGeom& g, int traced_tile_rows, int64_t* wire_bytes,
+                       void* stage, void* stream);
 // every rank's wire (rank r's at gathered + r * rank_stride) -> frames.  One launch.
 int launch_decode_gathered(const unsigned char* gathered, size_t rank_stride, int32_t* frames, const CodecGeom& g,
                            void* stream);

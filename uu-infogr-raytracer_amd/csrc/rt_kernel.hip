@@ -24,6 +24,7 @@
 #include <hip/hip_runtime.h>
 
 #include "rt_fastmath.h"
+#include "rt_codec_common.h"
 #include "rt_internal.h"
 
 // One wave (64 lanes, an 8x8 pixel tile) per workgroup: a one-wave group releases its LDS
@@ -210,6 +211,50 @@ __device__ __forceinline__ void store_pixel(const LaunchParams& p, int r, int y,
         o[0] = (unsigned char)px32;
         o[1] = (unsigned char)(px32 >> 8);
         o[2] = (unsigned char)(px32 >> 16);
+    }
+}
+
+// OUT_TILES: the tile codec's encoder (rt_codec.hip encode_group, format raytracer_hip/tilecodec.py)
+// fused into the trace -- the wave's 8x8 tile (lane = ry * 8 + rx) goes straight from registers to
+// its tile header and staged segments, and the band set never reaches HBM.  Converged call.
+// Residuals: dx = p - left (column 0: p - the tile's first pixel), minus the row above's dx (lane
+// - 8); widths from the wave OR; a row's w bytes of a segment are the OR of its 8 lanes' fields.
+__device__ __forceinline__ void encode_tile_fused(const LaunchParams& p, uint32_t px, bool valid) {
+    const int lane = threadIdx.x & 63, rx = lane & 7, ry = lane >> 3;
+    // (cross-lane steps by DPP / bpermute, so that the tile's values stay in VGPRs: readlanes
+    // here would raise the direct kernel's SGPR peak above 80 and cost it a wave per SIMD)
+    const uint32_t v = valid ? px & 0xffffffu : 0u;
+    const uint32_t first = (uint32_t)__shfl((int)v, 0, 64);
+    const size_t t = (size_t)(p.enc_frame0 + (int)blockIdx.z) * (size_t)p.enc_tpf +
+                     (size_t)blockIdx.y * (size_t)p.enc_tiles_x + blockIdx.x;
+    if (__builtin_amdgcn_ballot_w64(valid && v != first) == 0) {  // one colour (sky): no residual
+        if (lane == 0) wire_tile_hdr(p.enc_wire)[t] = first;
+        return;
+    }
+    const uint32_t left = row_shr<1>(v);  // lane - 1: the same row for rx >= 1
+    const uint32_t dx = sub_bytes(v, rx ? left : first);
+    const uint32_t above = (uint32_t)__shfl_up((int)dx, 8, 64);  // lane - 8: the row above
+    const uint32_t z = valid ? zigzag_bytes(ry ? sub_bytes(dx, above) : dx) & 0xffffffu : 0u;
+    uint32_t o = group8_or(z);  // the tile's OR, in every lane
+    o |= (uint32_t)__shfl_xor((int)o, 8, 64);
+    o |= (uint32_t)__shfl_xor((int)o, 16, 64);
+    o |= (uint32_t)__shfl_xor((int)o, 32, 64);
+    const uint32_t iR = width_index((o >> 16) & 0xffu), iG = width_index((o >> 8) & 0xffu),
+                   iB = width_index(o & 0xffu);
+    const uint32_t wm = width_at(iR) | (width_at(iG) << 4) | (width_at(iB) << 8);
+    if (lane == 0) wire_tile_hdr(p.enc_wire)[t] = first | ((iR + 6u * iG + 36u * iB) << 24);
+    if (wm) {  // (the same in every lane)
+        unsigned char* seg = (unsigned char*)(p.enc_stage + t * STAGE_WORDS);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const uint32_t w = (wm >> (4 * c)) & 15u;
+            if (w) {
+                const uint64_t f = (uint64_t)((z >> (16 - 8 * c)) & 0xffu) << (rx * w);
+                const uint32_t lo = group8_or((uint32_t)f), hi = group8_or((uint32_t)(f >> 32));
+                if (rx == 0) store_row_bits(seg + ry * w, w, ((uint64_t)hi << 32) | lo);
+            }
+            seg += 8 * w;
+        }
     }
 }
 
@@ -648,7 +693,7 @@ __device__ __forceinline__ Hit terminal_direct(const LaunchParams& p, f3 o, f3 d
 
 // DIRECT path, one 8x8 tile: each lane walks its own chain with per-lane (divergent) control
 // flow.  Returns the lane's packed counts: reflected segments (bits 0-7) | shadow rays << 8.
-template <int K, bool GPOW, typename T>
+template <int K, bool GPOW, bool TILES, typename T>
 __device__ __forceinline__ unsigned trace_tile_direct(const LaunchParams& p, int tile_x, float2* stk_lv, float* stk_dv,
                                                       T& tl) {
     const int lane = threadIdx.x & 63;
@@ -660,6 +705,7 @@ __device__ __forceinline__ unsigned trace_tile_direct(const LaunchParams& p, int
     unsigned cnt = 0;  // packed: reflected segments (bits 0-7) | shadow rays << CNT_SHADOW_SHIFT
     typename StackFor<K>::type stk(stk_lv, stk_dv);
     f3 leaf = mk(0.0f, 0.0f, 0.0f);
+    uint32_t px32 = 0;
     if (valid) {
         const f3 cam = mk(p.cam[0], p.cam[1], p.cam[2]);
         // TracePixel primary ray, :963-971 (no half-pixel offset)
@@ -709,21 +755,24 @@ __device__ __forceinline__ unsigned trace_tile_direct(const LaunchParams& p, int
             col = shade_direct<GPOW>(p, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z),
                                            mk(rb.x, rb.y, rb.z), ra.w, col, &cnt, tl);
         }
-        const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
-        store_pixel(p, r, y, x, px32);
+        px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
+        if constexpr (!TILES) store_pixel(p, r, y, x, px32);
     }
+    if constexpr (TILES) encode_tile_fused(p, px32, valid);
     return cnt;
 }
 
 // DIRECT kernel (scenes with < CULL_MIN_SPHERES spheres).
 // STATS: the diagnostic build that also tallies the work actually executed (not timed).
-template <int K, bool GPOW, bool STATS, int SMAX>
+// TILES: out_fmt OUT_TILES (the fused encoder: its own instantiation, so that the others keep their
+// register budget -- the epilogue alone raises the direct kernel's SGPR peak from 79 to 83).
+template <int K, bool GPOW, bool STATS, int SMAX, bool TILES>
 __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p) {
     constexpr int LDS_LEVELS = StackFor<K>::lds_levels;  // LdsStack slots, else unused
     __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
     __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * WG_THREADS : 1];
     Tally<STATS, SMAX> tl;
-    const unsigned cnt = trace_tile_direct<K, GPOW>(p, blockIdx.x, stk_lv, stk_dv, tl);
+    const unsigned cnt = trace_tile_direct<K, GPOW, TILES>(p, blockIdx.x, stk_lv, stk_dv, tl);
     add_counters<STATS>(p, threadIdx.x & 63, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
 }
 
@@ -1137,7 +1186,7 @@ __device__ __forceinline__ f3 fold_converged(const LaunchParams& p, STK& stk, f3
 
 // BUNDLE kernel (scenes with >= CULL_MIN_SPHERES spheres): converged control flow so that
 // every segment and every light can form a wave bundle and cull the sphere list.
-template <int K, bool GPOW, typename T>
+template <int K, bool GPOW, bool TILES, typename T>
 __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int tile_x, float2* stk_lv, float* stk_dv,
                                                       T& tl) {
     const int lane = threadIdx.x & 63;
@@ -1208,10 +1257,9 @@ __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int
     }
 
     const f3 col = fold_converged<GPOW>(p, stk, leaf, &cnt, tl);
-    if (valid) {
-        const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
-        store_pixel(p, r, y, x, px32);
-    }
+    const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
+    if constexpr (TILES) encode_tile_fused(p, px32, valid);
+    else if (valid) store_pixel(p, r, y, x, px32);
     return cnt;
 }
 
@@ -1221,22 +1269,22 @@ __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int
 // spilled to VGPR lanes) and 64 VGPRs (8 waves): C4 -2.6 %, C5 -7.5 %.  Not with GPOW (the f64
 // Math.Pow path would spill ~150 B/lane to scratch).  The direct kernel needs no cap (79 SGPRs, 48
 // VGPRs).
-template <int K, bool GPOW, bool STATS>
+template <int K, bool GPOW, bool STATS, bool TILES>
 __device__ __forceinline__ void bundle_kernel_body(const LaunchParams& p) {
     constexpr int LDS_LEVELS = StackFor<K>::lds_levels;  // LdsStack slots, else unused
     __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
     __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * WG_THREADS : 1];
     Tally<STATS> tl;
-    const unsigned cnt = trace_tile_bundle<K, GPOW>(p, blockIdx.x, stk_lv, stk_dv, tl);
+    const unsigned cnt = trace_tile_bundle<K, GPOW, TILES>(p, blockIdx.x, stk_lv, stk_dv, tl);
     add_counters<STATS>(p, threadIdx.x & 63, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
 }
-template <int K, bool STATS>
+template <int K, bool STATS, bool TILES>
 __global__ __launch_bounds__(WG_THREADS, 8) __attribute__((amdgpu_num_sgpr(80))) void trace_bundle_kernel(LaunchParams p) {
-    bundle_kernel_body<K, false, STATS>(p);
+    bundle_kernel_body<K, false, STATS, TILES>(p);
 }
-template <int K, bool STATS>
+template <int K, bool STATS, bool TILES>
 __global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel_gpow(LaunchParams p) {
-    bundle_kernel_body<K, true, STATS>(p);
+    bundle_kernel_body<K, true, STATS, TILES>(p);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1350,18 +1398,18 @@ static void launch_by_depth(const LaunchParams& p, dim3 grid, dim3 block, hipStr
     else if (need <= 8) hipLaunchKernelGGL(KERNEL<8>::fn, grid, block, 0, s, p);
     else hipLaunchKernelGGL(KERNEL<64>::fn, grid, block, 0, s, p);
 }
-template <bool GPOW, bool STATS, int SMAX>
+template <bool GPOW, bool STATS, int SMAX, bool TILES>
 struct DirectK {
     template <int K>
     struct at {
-        static constexpr auto fn = trace_direct_kernel<K, GPOW, STATS, SMAX>;
+        static constexpr auto fn = trace_direct_kernel<K, GPOW, STATS, SMAX, TILES>;
     };
 };
-template <bool GPOW, bool STATS>
+template <bool GPOW, bool STATS, bool TILES>
 struct BundleK {
     template <int K>
     struct at {
-        static constexpr auto fn = GPOW ? trace_bundle_kernel_gpow<K, STATS> : trace_bundle_kernel<K, STATS>;
+        static constexpr auto fn = GPOW ? trace_bundle_kernel_gpow<K, STATS, TILES> : trace_bundle_kernel<K, STATS, TILES>;
     };
 };
 
@@ -1369,11 +1417,12 @@ struct BundleK {
 // direct kernel whose sphere-pair loops are unrolled.
 constexpr int DIRECT_SMAX = 8;
 
-template <bool GPOW, bool STATS>
+template <bool GPOW, bool STATS, bool TILES = false>
 static void launch_variant(const LaunchParams& p, bool bundle, dim3 grid, dim3 block, hipStream_t s) {
-    if (bundle) launch_by_depth<BundleK<GPOW, STATS>::template at>(p, grid, block, s);
-    else if (p.S <= DIRECT_SMAX) launch_by_depth<DirectK<GPOW, STATS, DIRECT_SMAX>::template at>(p, grid, block, s);
-    else launch_by_depth<DirectK<GPOW, STATS, 0>::template at>(p, grid, block, s);
+    if (bundle) launch_by_depth<BundleK<GPOW, STATS, TILES>::template at>(p, grid, block, s);
+    else if (p.S <= DIRECT_SMAX)
+        launch_by_depth<DirectK<GPOW, STATS, DIRECT_SMAX, TILES>::template at>(p, grid, block, s);
+    else launch_by_depth<DirectK<GPOW, STATS, 0, TILES>::template at>(p, grid, block, s);
 }
 
 int launch_trace(const LaunchParams& p, bool generic_pow, bool stats, void* stream) {
@@ -1385,7 +1434,10 @@ int launch_trace(const LaunchParams& p, bool generic_pow, bool stats, void* stre
     // bundle culling pays for its per-wave bounds only with enough spheres (A/B: +15 % at
     // 8 spheres, 3x faster at 64)
     const bool bundle = p.S >= CULL_MIN_SPHERES;
-    if (stats) {
+    if (p.out_fmt == OUT_TILES) {  // the fused encoder (never with the diagnostic tallies)
+        if (generic_pow) launch_variant<true, false, true>(p, bundle, grid, block, s);
+        else launch_variant<false, false, true>(p, bundle, grid, block, s);
+    } else if (stats) {
         if (generic_pow) launch_variant<true, true>(p, bundle, grid, block, s);
         else launch_variant<false, true>(p, bundle, grid, block, s);
     } else {

@@ -185,6 +185,19 @@ class Context:
                                                 rank_stride, n_frames, C.c_void_p(d_frames), frame_stride,
                                                 C.c_void_p(stream)))
 
+    def render_bands_tiles(self, width: int, height: int, band_rows: int, rank: int, world: int, frame0: int,
+                           n_frames: int, batch_frames: int, d_wire: int, stream: int = 0):
+        """Frames frame0.. of a batch of `rank`'s bands traced straight into the wire's tile headers and
+        the context's codec scratch (rt_render_bands_tiles; rt_finish_wire completes the wire)."""
+        self._check(self.lib.rt_render_bands_tiles(self.ptr, width, height, band_rows, rank, world, frame0, n_frames,
+                                                   batch_frames, C.c_void_p(d_wire), C.c_void_p(stream)))
+
+    def finish_wire(self, width: int, height: int, band_rows: int, rank: int, world: int, n_frames: int,
+                    d_wire: int, d_wire_bytes: int = 0, stream: int = 0):
+        """The wire of the batch's first n_frames traced by render_bands_tiles (rt_finish_wire)."""
+        self._check(self.lib.rt_finish_wire(self.ptr, width, height, band_rows, rank, world, n_frames,
+                                            C.c_void_p(d_wire), C.c_void_p(d_wire_bytes or None), C.c_void_p(stream)))
+
     def render_async(self, width: int, height: int, out: np.ndarray):
         """Double-buffered Tick (rt_render_async): returns at once; `wait()` before reading `out`."""
         assert out.dtype == np.int32 and out.flags.c_contiguous and out.size == width * height

@@ -134,6 +134,10 @@ EXPORTS = [
                                   C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]),
     ("rt_decode_gathered", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_size_t,
                                      C.c_int, C.c_void_p, C.c_size_t, C.c_void_p]),
+    ("rt_render_bands_tiles", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                        C.c_int, C.c_void_p, C.c_void_p]),
+    ("rt_finish_wire", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
+                                 C.c_void_p, C.c_void_p]),
     ("rt_render_async", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     ("rt_wait", C.c_int, [C.c_void_p]),
     ("rt_write_ppm", C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),

@@ -283,7 +283,7 @@ class TileBandGather:
     """
 
     def __init__(self, rb: RowBands, device, frames_per_batch, layout_fn, encode, decode, rank0_codec=False,
-                 compositor=False, phys_rank=None, phys_world=None):
+                 compositor=False, phys_rank=None, phys_world=None, fused=False):
         import torch
         self.rb, self.F, self.device = rb, max(1, frames_per_batch), torch.device(device)
         self.cuda = self.device.type == "cuda"
@@ -299,11 +299,14 @@ class TileBandGather:
         self.first_rank = 0 if (rank0_codec or self.compositor) else 1
         self.direct = self.root and not rank0_codec and not self.compositor  # rank 0 renders into its frames
         self.idle = self.root and self.compositor  # rank 0 only assembles
+        # fused: this rank traces its bands straight into the wire of the batch (rt_render_bands_tiles;
+        # `wire_target`), and stage A's encode(None, ...) only finishes that wire (rt_finish_wire)
+        self.fused = bool(fused) and not (self.direct or self.idle)
         self.slot_elems = rb.slot_elems
         lay = layout_fn(self.F)
         self.rank_stride = (int(lay.max_bytes) + 255) // 256 * 256
         self.raw = ([torch.zeros(self.F * self.slot_elems, dtype=torch.int32, device=self.device) for _ in range(2)]
-                    if not (self.direct or self.idle) else None)
+                    if not (self.direct or self.idle or self.fused) else None)
         self.wire = [torch.zeros(self.rank_stride, dtype=torch.uint8, device=self.device) for _ in range(3)]
         self.size = [torch.zeros(1, dtype=torch.int64, device=self.device) for _ in range(3)]
         self.size_host = torch.zeros(3, dtype=torch.int64, pin_memory=self.cuda)
@@ -384,10 +387,19 @@ class TileBandGather:
     def ring_of(self, batch):
         return self.frames[batch % 3]
 
+    def wire_target(self, k=None):
+        """Fused mode: the wire that frame k's batch is traced into."""
+        k = self.k if k is None else k
+        if not self.fused:
+            raise RuntimeError("wire_target needs fused mode")
+        return self.wire[(k // self.F) % 3]
+
     def target(self, k=None):
         k = self.k if k is None else k
         if self.idle:
             raise RuntimeError("the compositor rank traces nothing")
+        if self.fused:
+            raise RuntimeError("fused mode: trace into wire_target()")
         if self.direct:
             o = (k % self.F) * self.frame_elems
             return self.frames[(k // self.F) % 3][o:o + self.frame_elems]
@@ -407,6 +419,10 @@ class TileBandGather:
             self._stage_c()
         if self.direct and b - 3 in self.decoded_ev and self.cuda:
             ev = self.decoded_ev[b - 3]
+            for st in streams:
+                st.wait_event(ev)
+        if self.fused and b - 3 in self.gathered_ev and self.cuda:  # the trace writes wire b % 3,
+            ev = self.gathered_ev[b - 3]                           # last read by gather b-3
             for st in streams:
                 st.wait_event(ev)
 
@@ -435,7 +451,7 @@ class TileBandGather:
         if self.direct or self.idle:
             self.size[i].zero_()  # nothing to ship: rank 0's bands are in its frames (or it has none)
         else:
-            self.encode(self.raw[b % 2], n_frames, self.wire[i], self.size[i], main)
+            self.encode(None if self.fused else self.raw[b % 2], n_frames, self.wire[i], self.size[i], main)
         if self.cuda:  # (events reused round robin: a wait takes the state recorded before it)
             ev = self.enc_events[b % len(self.enc_events)]
             ev.record(main)
