@@ -139,12 +139,12 @@ def test_gloo_tile_encoded_gather(tmp_path, world, frames, per_batch, rank0_code
     """bench.py's default N>1 step: tile-encoded band sets, size all_reduce + gather, three-stage
     pipeline; every frame decodes to its own oracle frame, the last batch may be partial.  With
     `compositor` (bench.py at N >= 8) rank 0 traces nothing and decodes every band set.  With
-    `speculate`, after the first batch the gathers use speculative sizes (set_capacity(margin));
-    margins below 1 force batches to be gathered again at their reduced size.  With `after_drain`
-    the pipeline is drained before the switch (as bench.py's warm-up): the next batch finds it
-    empty and takes the gather-first path (decode before the size check, a second gather and
-    decode when the guess was short); with 5 frames in batches of 2 that batch is the last,
-    partial one, as in a short run."""
+    `speculate`, set_capacity(margin) is called after the first two batches: batches inside the
+    pipeline keep their exact sizes.  With `after_drain` the pipeline is drained before the switch
+    (as bench.py's warm-up): the next batch finds it empty and takes the speculative gather-first
+    path (decode before the size check; margins below 1 force a second gather and decode at the
+    reduced size); with 5 frames in batches of 2 that batch is the last, partial one, as in a
+    short run."""
     import dist_worker
     ctx = mp.get_context("spawn")
     port = _free_port()

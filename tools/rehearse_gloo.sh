@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 port=29611
-for spec in "2 auto C2 --batch 16" "3 auto C3 --batch 8" "4 on C2 --batch 16" "4 off C3 --batch 16 --band-format rgb24" "2 auto C2 --batch 16 --rank0-codec"; do
+for spec in "2 auto C2 --batch 16" "3 auto C3 --batch 8" "4 on C2 --batch 16" "4 off C3 --batch 16 --band-format rgb24" "2 auto C2 --batch 16 --rank0-codec" "3 on C4 --batch 8 --no-fuse"; do
     set -- $spec
     n=$1; comp=$2; cfg=$3; shift 3
     port=$((port + 1))

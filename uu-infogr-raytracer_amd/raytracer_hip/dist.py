@@ -253,14 +253,13 @@ class TileBandGather:
     decode b-3 filled it -- `begin_batch`).  With gloo on CPU tensors (tests) the same
     sequence runs synchronously.
 
-    Speculative mode (`set_capacity`, bench.py after its warm-up): a batch's gather size is a
-    guess (1.25 x the largest wire per frame so far), so stage B gathers without waiting for the
-    size, and stage C checks the reduced size before the decode; a batch whose largest wire
-    outgrew the guess is gathered again in full (every rank sees the same reduced size, so all of
-    them take part).  A batch that finds the pipeline empty (a run's first batch -- all of a
-    short run) goes further: its gather is issued in stage A right behind the encode, the size
-    reduce after it, and stage C decodes before it reads the size (decoding again after a second
-    gather), so neither the reduce nor the host's read-back sits between encode and decode.
+    Speculative mode (`set_capacity`, bench.py after its warm-up) for a batch that finds the
+    pipeline empty (a run's first batch -- all of a short run): its gather size is a guess (1.25 x
+    the largest wire per frame so far), issued in stage A right behind the encode, the size reduce
+    after it, and stage C decodes before it reads the reduced size -- neither the reduce nor the
+    host's read-back sits between encode and decode.  A batch whose largest wire outgrew the
+    guess is gathered again in full and decoded again (every rank sees the same reduced size, so
+    all of them take part).  Batches inside a pipeline keep the exact size of stage B.
 
         g.begin_batch(streams)      -> before frame k when k % F == 0 (rank 0: ring reuse)
         dst = g.target(k)           -> rank 0 direct: int32 view of frame k's ring slot (render
@@ -476,12 +475,9 @@ class TileBandGather:
             self._stage_c()
         b, n_frames, work = self.stage_b.pop(0)
         i = b % 3
-        if self.capacity_per_frame is not None:
-            # speculative size: gather now, check the reduced size in stage C (before the decode:
-            # by then the reduce has long completed)
-            n = self._spec_bytes(n_frames)
-            self.stage_c.append((b, n_frames, self._gather(b, i, n), (work, n, False)))
-            return
+        # (the exact size even with set_capacity: in a pipeline the reduce of batch b-1 completed
+        # while batch b was traced, and a speculative gather would move the margin over the links
+        # too -- world-1 rehearsal at 1024 frames: 19.9-20.0 us/frame exact, 20.5-20.7 speculative)
         n = self._read_size(i, work)
         self.max_per_frame = max(self.max_per_frame, n / n_frames)
         self.bytes_sent += n
