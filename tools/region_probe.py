@@ -23,8 +23,15 @@ def main():
     ap.add_argument("--order", default="0s,1s,0p,0s,1s,0p",
                     help="variants measured in this order: rt_set_timing value + s (torch.cuda.synchronize) "
                          "or p (poll the closing event, then synchronize)")
+    ap.add_argument("--spin", action="store_true",
+                    help="hipSetDeviceFlags(hipDeviceScheduleSpin) before the first GPU call: the host spins on "
+                         "completion instead of yielding / sleeping")
     a = ap.parse_args()
     import torch
+    if a.spin:  # torch's HIP runtime (same soname), before anything initialises the device
+        import ctypes
+        rc = ctypes.CDLL("libamdhip64.so.7").hipSetDeviceFlags(1)
+        print(f"hipSetDeviceFlags(hipDeviceScheduleSpin) -> {rc}")
     from raytracer_hip import Context, abi, scenes
     sc = scenes.config(a.config)
     W, H, F = sc.width, sc.height, a.frames
@@ -79,7 +86,7 @@ def main():
         ev1.record(st)
         torch.cuda.synchronize()
         rows.append(time.perf_counter() - t0)
-    print(f"empty region (two event records + sync): wall {stx.median(rows) * 1e6:.1f} us")
+    print(f"empty region (two event records + sync{', spin' if a.spin else ''}): wall {stx.median(rows) * 1e6:.1f} us")
 
 
 if __name__ == "__main__":
