@@ -133,7 +133,10 @@ def test_scatter_gathered_host_matches_scatter_host():
                           (2, 4, 4, False, True, 0, False), (2, 9, 2, False, False, 1.25, False),
                           (3, 9, 2, False, True, 0.5, False), (2, 8, 2, True, False, 0.25, False),
                           (2, 5, 2, False, False, 0.25, True), (3, 9, 2, False, True, 1.25, True),
-                          (3, 9, 2, True, False, 0.5, True)])
+                          (3, 9, 2, True, False, 0.5, True),
+                          # the driver's N = 8 shape: compositor, a short run as one batch after the
+                          # warm-up drained the pipeline (speculative gather-first path)
+                          (8, 5, 5, False, True, 1.25, True)])
 def test_gloo_tile_encoded_gather(tmp_path, world, frames, per_batch, rank0_codec, compositor, speculate,
                                   after_drain):
     """bench.py's default N>1 step: tile-encoded band sets, size all_reduce + gather, three-stage
