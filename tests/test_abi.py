@@ -202,3 +202,23 @@ def test_ctypes_layouts_match_the_c_header(tmp_path):
         assert int(got[n]) == C.sizeof(t), n
         for f, _ in t._fields_:
             assert int(got[f"{n}.{f}"]) == getattr(t, f).offset, f"{n}.{f}"
+
+
+def test_bit_pattern_selection_rule():
+    """rt_kernel.hip take_primary / take_secondary select on bit patterns: with u(x) = bits(x) - 1
+    (uint32, wrapping), `x > 0 && x < best` == `u(x) < u(best)` whenever best is +inf or a positive
+    float (the only values a nearest-hit search holds).  Checked on every special value and on
+    random bit patterns against the IEEE comparison."""
+    rng = np.random.default_rng(7)
+    special = np.array([0x00000000, 0x80000000, 0x00000001, 0x80000001, 0x007fffff, 0x00800000, 0x3f800000,
+                        0xbf800000, 0x7f7fffff, 0xff7fffff, 0x7f800000, 0xff800000, 0x7f800001, 0x7fc00000,
+                        0x7fffffff, 0xff800001, 0xffc00000, 0xffffffff], dtype=np.uint32)
+    xs = np.concatenate([special, rng.integers(0, 2**32, 200_000, dtype=np.uint64).astype(np.uint32)])
+    pos = xs[(xs.view(np.float32) > 0) & np.isfinite(xs.view(np.float32))]
+    bests = np.concatenate([np.array([0x7f800000], dtype=np.uint32), special[[2, 4, 5, 6, 8]], pos[:300]])
+    u = lambda b: (b.astype(np.uint64) - 1) % 2**32  # noqa: E731
+    with np.errstate(invalid="ignore"):
+        for b in bests:
+            bf = np.array([b], dtype=np.uint32).view(np.float32)[0]
+            ref = (xs.view(np.float32) > 0) & (xs.view(np.float32) < bf)
+            assert np.array_equal(ref, u(xs) < u(np.array([b], dtype=np.uint32))[0]), hex(int(b))

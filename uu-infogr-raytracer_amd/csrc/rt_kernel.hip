@@ -435,20 +435,24 @@ struct Hit {
 };
 constexpr int HIT_NONE = 0x7fffffff;
 
-// Nearest-hit selection rules as selects (VALU compares and cndmasks, no scalar mask logic):
+// Nearest-hit selection rules as selects (VALU compares and cndmasks, no scalar mask logic),
+// on the bit patterns: with u(x) = bits(x) - 1 (unsigned, wrapping), +0, every negative value and
+// every NaN map above u(+inf) = 0x7f7fffff, and positive floats keep their order.  `best` is
+// always +inf or a taken positive distance, so "x > 0 && x < best" is exactly u(x) < u(best)
+// (x = +inf: u(x) = u(+inf) >= u(best), not taken, as in the float rule) -- one compare and a
+// min instead of two compares and two selects (C4 -0.5 %, C2/C3 +-0,
+// profiles/ab/r02_umin_take.txt).
 // TracePixel (:977, :987): t is taken iff t > 0 && best > t.
 __device__ __forceinline__ void take_primary(float t, int i, float& best, int& win) {
-    const float tt = t > 0.0f ? t : __builtin_inff();
-    const bool b = tt < best;
-    best = b ? tt : best;
-    win = b ? i : win;
+    const unsigned u = __float_as_uint(t) - 1u, ub = __float_as_uint(best) - 1u;
+    win = u < ub ? i : win;
+    best = __uint_as_float(min(u, ub) + 1u);
 }
 // TraceSecondaryRay (:804-806): t is taken iff t - 0.01 > 0 && t - 0.01 < best, and then
 // best = t (the asymmetric rule, Q5/Q6).
 __device__ __forceinline__ void take_secondary(float t, int i, float& best, int& win) {
     const float tm = t - 0.01f;
-    const float tt = tm > 0.0f ? tm : __builtin_inff();
-    const bool b = tt < best;
+    const bool b = __float_as_uint(tm) - 1u < __float_as_uint(best) - 1u;
     best = b ? t : best;
     win = b ? i : win;
 }
