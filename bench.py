@@ -824,6 +824,23 @@ def main_single(args, torch, Context, abi, scenes):
             ctx.render(W, H, host)
         out["tick_fps_incl_d2h"] = n_tick / (time.perf_counter() - t1)
         ctx.unregister_host(host)
+        # the double-buffered Tick (rt_render_async: trace stream + copy stream, two device frames):
+        # frame k+1's trace overlaps frame k's D2H; a display loop keeps two frames in flight and
+        # waits for the pair (deeper queues of D2H copies measured slower: tools/tick_probe.py)
+        hosts = [np.empty(W * H, dtype=np.int32) for _ in range(2)]
+        for hb in hosts:
+            ctx.register_host(hb)
+        ctx.render_async(W, H, hosts[0])
+        ctx.wait()
+        t1 = time.perf_counter()
+        for k in range(n_tick):
+            ctx.render_async(W, H, hosts[k % 2])
+            if k % 2:
+                ctx.wait()
+        ctx.wait()
+        out["tick_async_fps_incl_d2h"] = n_tick / (time.perf_counter() - t1)
+        for hb in hosts:
+            ctx.unregister_host(hb)
     also = [c for c in (x.strip() for x in args.also.split(",")) if c and c.upper() != sc.name.upper()]
     if also:
         out["also"] = {}

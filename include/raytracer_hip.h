@@ -285,10 +285,10 @@ int rt_finish_wire(rt_ctx* ctx, int width, int height, int band_rows, int rank, 
  * into the caller's host buffer pixels[width*height] and returns at once.  rt_wait blocks
  * until every enqueued frame is complete.  With two host buffers a caller overlaps the
  * trace of frame k+1 with its own use of frame k (the camera of k+1 can already be set).
- * The context keeps two device frame buffers, each with its own stream, so two frames are
- * in flight: frame k+1's trace fills the GPU while frame k's last waves finish (measured
- * 17-26 % more frames/s than back-to-back launches).  Frames on the same buffer complete
- * in order; rt_wait returns when every enqueued frame is complete.
+ * The context keeps two device frame buffers, a trace stream and a copy stream: frame k+1's
+ * trace overlaps frame k's D2H copy (1080p C2: 190 us per frame with two frames in flight
+ * and an rt_wait per pair, against 200 us for rt_render).  Frames complete in order;
+ * rt_wait returns when every enqueued frame is complete.
  * Multi-GPU contexts render synchronously here (rt_render). */
 int rt_render_async(rt_ctx* ctx, int width, int height, int32_t* pixels);
 int rt_wait(rt_ctx* ctx);
