@@ -41,6 +41,14 @@ def main():
     rate("async, one buffer, one wait", lambda m: asy(m, 0, False))
     rate("async, alternating, wait every frame", lambda m: asy(m, 1, True))
     rate("async, alternating, wait every 2 frames", lambda m: asy(m, 2, True))
+    # the same deep queue into hipHostMalloc'd memory (torch pinned tensors) instead of registered memory
+    pinned = [torch.empty(W * H, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+
+    def asy_pinned(m):
+        for k in range(m):
+            ctx.lib.rt_render_async(ctx.ptr, W, H, pinned[k % 2].data_ptr())
+        ctx.wait()
+    rate("async into hipHostMalloc memory, one wait", asy_pinned)
     # the bare copy: 8.3 MB device -> pinned host through torch
     src = torch.empty(W * H, dtype=torch.int32, device="cuda")
     dst = torch.empty(W * H, dtype=torch.int32, pin_memory=True)
