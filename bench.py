@@ -103,7 +103,7 @@ def parse(argv=None):
                          "one GPU).  Exercises every rank's code path (bands, codec, pipelined gathers, compositor, "
                          "barrier and max-over-ranks timing); the line is marked 'rehearsal' and is not a result")
     ap.add_argument("--cpu-seconds", type=float, default=20.0,
-                    help="CPU baseline budget: about half on the bench config, the rest on C1 and the verbatim "
+                    help="CPU baseline budget: 40 %% on the bench config, the rest on C3, C1 and the verbatim "
                          "reference scene")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-tick", action="store_true",
@@ -319,6 +319,65 @@ def single_summary(sc, m, steps):
         "frame_period_ms": m["period_s"] * 1e3, "hbm_gbs": achieved, "hbm_frac": achieved / HBM_PEAK_GBS,
         "f_alg": OPS_PER_SPHERE_TEST * st["sphere_tests"] + OPS_PER_PLANE_TEST * st["plane_tests"],
     }
+
+
+def tick_rates(ctx, W, H, torch, n=20, reps=3):
+    """The interactive shapes beside the batched headline (never `value`); each the median of
+    `reps` runs of n frames, same camera:
+    - single_launch_fps: rt_render_device, one frame per launch, device-resident (what a Tick()
+      loop issues, without the PCIe hand-off);
+    - tick_fps_incl_d2h: rt_render, the synchronous Tick() (trace + D2H into the caller's
+      registered buffer, returns with the frame complete);
+    - tick_async_fps_incl_d2h: rt_render_async into two alternating registered buffers and an
+      rt_wait per pair (a display loop two frames deep);
+    - tick_async_deep_fps_incl_d2h: n frames queued into n registered buffers, one rt_wait.
+    rt_render_async's D2H of frame k rides in frame k+1's launch (copy slice) or rt_wait's."""
+    import numpy as np
+
+    def med(fn):
+        fn()  # warm
+        rates = []
+        for _ in range(reps):
+            t = time.perf_counter()
+            fn()
+            rates.append(n / (time.perf_counter() - t))
+        return sorted(rates)[len(rates) // 2], [round(r, 1) for r in rates]
+
+    dev = torch.empty(W * H, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream()
+
+    def single():
+        for _ in range(n):
+            ctx.render_device(W, H, dev.data_ptr(), st.cuda_stream)
+        torch.cuda.synchronize()
+    hosts = [np.zeros(W * H, dtype=np.int32) for _ in range(n)]
+    for hb in hosts:
+        ctx.register_host(hb)
+
+    def sync():
+        for _ in range(n):
+            ctx.render(W, H, hosts[0])
+
+    def pair():
+        for k in range(n):
+            ctx.render_async(W, H, hosts[k % 2])
+            if k % 2:
+                ctx.wait()
+        ctx.wait()
+
+    def deep():
+        for k in range(n):
+            ctx.render_async(W, H, hosts[k])
+        ctx.wait()
+    out = {}
+    for key, fn in (("single_launch_fps", single), ("tick_fps_incl_d2h", sync), ("tick_async_fps_incl_d2h", pair),
+                    ("tick_async_deep_fps_incl_d2h", deep)):
+        out[key], out[key + "_runs"] = med(fn)
+    for hb in hosts:
+        ctx.unregister_host(hb)
+    out["tick_note"] = (f"median of {reps} runs of {n} frames each; single_launch_fps = rt_render_device one frame per "
+                        f"launch into HBM; tick_* include the D2H into registered host memory (PCIe)")
+    return out
 
 
 def main():
@@ -813,34 +872,7 @@ def main_single(args, torch, Context, abi, scenes):
                                      note="nominal counts (SURVEY.md 8d: every primitive of every visible-path ray) "
                                           "vs *_run = exact tests / shadow rays the kernel executed (skipped: shadow "
                                           "tests that cannot change the pixel, culled spheres)")
-        # Tick() path for context: full frame into pinned host memory (PCIe D2H included); not `value`
-        import numpy as np
-        host = np.empty(W * H, dtype=np.int32)
-        ctx.register_host(host)
-        ctx.render(W, H, host)
-        n_tick = 20
-        t1 = time.perf_counter()
-        for _ in range(n_tick):
-            ctx.render(W, H, host)
-        out["tick_fps_incl_d2h"] = n_tick / (time.perf_counter() - t1)
-        ctx.unregister_host(host)
-        # the double-buffered Tick (rt_render_async: trace stream + copy stream, two device frames):
-        # frame k+1's trace overlaps frame k's D2H; a display loop keeps two frames in flight and
-        # waits for the pair (deeper queues of D2H copies measured slower: tools/tick_probe.py)
-        hosts = [np.empty(W * H, dtype=np.int32) for _ in range(2)]
-        for hb in hosts:
-            ctx.register_host(hb)
-        ctx.render_async(W, H, hosts[0])
-        ctx.wait()
-        t1 = time.perf_counter()
-        for k in range(n_tick):
-            ctx.render_async(W, H, hosts[k % 2])
-            if k % 2:
-                ctx.wait()
-        ctx.wait()
-        out["tick_async_fps_incl_d2h"] = n_tick / (time.perf_counter() - t1)
-        for hb in hosts:
-            ctx.unregister_host(hb)
+        out.update(tick_rates(ctx, W, H, torch))
     also = [c for c in (x.strip() for x in args.also.split(",")) if c and c.upper() != sc.name.upper()]
     if also:
         out["also"] = {}
@@ -852,8 +884,15 @@ def main_single(args, torch, Context, abi, scenes):
                                                         "workload", "kernel", "kernel_avg_ms", "kernel_ms_per_frame",
                                                         "frames_per_launch", "launches", "hbm_frac")}
     if not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline([(sc, r["rays_per_frame"], 0.5), (scenes.config("C1"), None, 0.2),
-                                            (scenes.reference(512, 512), None, 0.3)], args.cpu_seconds)
+        # the bench config, then C3 (the north-star config: 1080p with reflections), C1
+        # (BASELINE configs[0]) and the verbatim reference scene beside it
+        c3 = scenes.config("C3")
+        c3_rays = out.get("also", {}).get("C3", {}).get("rays_per_frame")
+        cpu_samples = [(sc, r["rays_per_frame"], 0.4)]
+        if sc.name.upper() != "C3":
+            cpu_samples.append((c3, c3_rays, 0.25))
+        cpu_samples += [(scenes.config("C1"), None, 0.15), (scenes.reference(512, 512), None, 0.2)]
+        out["cpu_baseline"] = cpu_baseline(cpu_samples, args.cpu_seconds)
     print(json.dumps(out), flush=True)
     ctx.close()
 

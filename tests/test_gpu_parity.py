@@ -274,7 +274,7 @@ def test_render_async_double_buffered_frames(oracle):
         for k, (pos, yaw, pitch) in enumerate(cams):
             ctx.set_camera(abi.rt_camera(abi.rt_vec3(*pos), yaw, pitch))
             ctx.render_async(W, H, bufs[k % 2])
-            if k >= 1:  # frame k-1 is read while frame k traces (wait covers both: in-order stream)
+            if k >= 1:  # frame k-1 is read after frame k is queued (rt_wait completes both: one in-order stream)
                 ctx.wait()
                 got.append(bufs[(k - 1) % 2].reshape(H, W).copy())
         ctx.wait()
@@ -286,6 +286,106 @@ def test_render_async_double_buffered_frames(oracle):
         s2.camera = (pos, float(np.float32(yaw)), float(np.float32(pitch)))
         want, _ = oracle.render(s2, oracle.MODE_NEAREST, 4)
         assert_same(got[k], want, f"async frame {k}")
+
+
+def _oracle_frame(oracle, W, H, cam):
+    pos, yaw, pitch = cam
+    s2 = scenes.reference(W, H)
+    s2.camera = (pos, float(np.float32(yaw)), float(np.float32(pitch)))
+    return oracle.render(s2, oracle.MODE_NEAREST, 4)[0]
+
+
+def test_render_async_deep_queue_one_wait(oracle):
+    """rt_render_async under load -- 9 frames queued with a new camera each, each into
+    its own registered host buffer, and one rt_wait at the end; the frame size changes twice
+    mid-queue (reallocation of the device double buffer).  Frame k's copy rides in frame k+1's
+    launch (the copy slice), so a missing or misplaced ordering shows up as a wrong frame."""
+    sizes = [(96, 72)] * 4 + [(130, 66)] * 3 + [(33, 17), (96, 72)]
+    cams = [((0.1 * k, 0.05 * k, -0.2 * k), 0.07 * k, -0.03 * k) for k in range(len(sizes))]
+    bufs = [np.full(w * h, 0x7f7f7f7f, dtype=np.int32) for w, h in sizes]
+    with Context(1) as ctx:
+        ctx.set_scene(scenes.reference(96, 72))
+        for b in bufs:
+            ctx.register_host(b)
+        for (w, h), cam, b in zip(sizes, cams, bufs):
+            ctx.set_camera(abi.rt_camera(abi.rt_vec3(*cam[0]), cam[1], cam[2]))
+            ctx.render_async(w, h, b)
+        ctx.wait()
+        got = [b.reshape(h, w).copy() for (w, h), b in zip(sizes, bufs)]
+        for b in bufs:
+            ctx.unregister_host(b)
+    for k, ((w, h), cam) in enumerate(zip(sizes, cams)):
+        assert_same(got[k], _oracle_frame(oracle, w, h, cam), f"queued async frame {k} ({w}x{h})")
+
+
+def test_render_async_full_hd_deep_queue(oracle):
+    """The bench's Tick shape at 1920x1080: 5 queued frames, 2 alternating registered buffers
+    would be overwritten, so 5 buffers; one wait; every frame = the oracle's for its camera."""
+    W, H = 1920, 1080
+    cams = [((0.0, 0.1 * k, -0.3 * k), 0.05 * k, 0.02 * k) for k in range(5)]
+    bufs = [np.zeros(W * H, dtype=np.int32) for _ in cams]
+    with Context(1) as ctx:
+        ctx.set_scene(scenes.reference(W, H))
+        for b in bufs:
+            ctx.register_host(b)
+        for cam, b in zip(cams, bufs):
+            ctx.set_camera(abi.rt_camera(abi.rt_vec3(*cam[0]), cam[1], cam[2]))
+            ctx.render_async(W, H, b)
+        ctx.wait()
+        got = [b.reshape(H, W).copy() for b in bufs]
+        for b in bufs:
+            ctx.unregister_host(b)
+    for k, cam in enumerate(cams):
+        assert_same(got[k], _oracle_frame(oracle, W, H, cam), f"1080p async frame {k}")
+
+
+def test_render_async_unregistered_and_pinned_buffers(oracle):
+    """Buffers not registered through rt_register_host (pageable numpy memory, torch's
+    hipHostMalloc'd pinned memory) take hipMemcpyAsync on the same stream, never the copy slice:
+    mixed in one queue with a registered buffer, every frame is right."""
+    import torch
+    W, H = 80, 60
+    cams = [((0.0, 0.0, -0.1 * k), 0.1 * k, 0.0) for k in range(4)]
+    reg = np.zeros(W * H, dtype=np.int32)
+    pinned = torch.zeros(W * H, dtype=torch.int32, pin_memory=True)
+    bufs = [np.zeros(W * H, dtype=np.int32), reg, pinned.numpy(), np.zeros(W * H, dtype=np.int32)]
+    with Context(1) as ctx:
+        ctx.set_scene(scenes.reference(W, H))
+        ctx.register_host(reg)
+        for cam, b in zip(cams, bufs):
+            ctx.set_camera(abi.rt_camera(abi.rt_vec3(*cam[0]), cam[1], cam[2]))
+            ctx.render_async(W, H, b)
+        ctx.wait()
+        got = [b.reshape(H, W).copy() for b in bufs]
+        ctx.unregister_host(reg)
+    for k, cam in enumerate(cams):
+        assert_same(got[k], _oracle_frame(oracle, W, H, cam), f"async frame {k}")
+
+
+def test_render_async_pending_frame_flushed_by_unregister_and_render(oracle):
+    """A frame whose copy is still pending is written before rt_unregister_host releases its
+    buffer and before a synchronous rt_render (which may reuse the buffer) runs."""
+    W, H = 64, 48
+    cam0, cam1 = ((0.2, 0.0, -0.5), 0.1, 0.05), ((-0.2, 0.1, -0.4), -0.1, 0.0)
+    a = np.zeros(W * H, dtype=np.int32)
+    b = np.zeros(W * H, dtype=np.int32)
+    with Context(1) as ctx:
+        ctx.set_scene(scenes.reference(W, H))
+        ctx.register_host(a)
+        ctx.register_host(b)
+        ctx.set_camera(abi.rt_camera(abi.rt_vec3(*cam0[0]), cam0[1], cam0[2]))
+        ctx.render_async(W, H, a)
+        ctx.unregister_host(a)  # no rt_wait: the pending copy must land first
+        got_a = a.reshape(H, W).copy()
+        ctx.render_async(W, H, b)  # cam0 again, pending into b
+        ctx.set_camera(abi.rt_camera(abi.rt_vec3(*cam1[0]), cam1[1], cam1[2]))
+        ctx.render(W, H, b)  # the synchronous Tick into the same buffer: its frame must win
+        got_b = b.reshape(H, W).copy()
+        ctx.wait()
+        assert np.array_equal(b.reshape(H, W), got_b), "a flushed async frame overwrote rt_render's"
+        ctx.unregister_host(b)
+    assert_same(got_a, _oracle_frame(oracle, W, H, cam0), "frame pending at rt_unregister_host")
+    assert_same(got_b, _oracle_frame(oracle, W, H, cam1), "rt_render after a pending async frame")
 
 
 @pytest.mark.parametrize("cid,w,h", [("REF", 96, 64), ("C3", 80, 45), ("C4", 64, 36)])

@@ -86,11 +86,15 @@ struct Device {
     size_t stage_cap = 0;
     int32_t* d_frames2[2] = {nullptr, nullptr};  // rt_render_async double buffer
     size_t frames2_cap[2] = {0, 0};
-    // rt_render_async: slot_stream[0] traces, slot_stream[1] copies (one copy stream: the D2H
-    // copies of consecutive frames never run side by side); traced_ev[b] / copied_ev[b] order
-    // buffer b's trace before its copy and its next trace after that copy
-    hipStream_t slot_stream[2] = {nullptr, nullptr};
-    hipEvent_t traced_ev[2] = {nullptr, nullptr}, copied_ev[2] = {nullptr, nullptr};
+    // rt_render_async: one in-order stream; frame k's D2H rides in frame k+1's launch (the copy
+    // slice, LaunchParams::copy_words) or is issued by rt_wait -- `hand` is that pending copy
+    hipStream_t async_stream = nullptr;
+    struct {
+        int32_t* host = nullptr;       // caller's buffer
+        int32_t* mapped = nullptr;     // its device-mapped address (rt_register_host)
+        const int32_t* src = nullptr;  // d_frames2[slot]
+        size_t words = 0;
+    } hand;
     float* d_view_tab = nullptr;  // lx[W] then ly[H] (view_tables)
     size_t view_tab_cap = 0;
     int tab_w = -1, tab_h = -1;
@@ -126,6 +130,14 @@ struct rt_ctx {
     uint64_t timed[3] = {0, 0, 0};  // timed launches, copies, gathers
     int timing_every = 64;
     int32_t* host_staging = nullptr;
+    // host ranges registered through rt_register_host and their device-mapped addresses: only
+    // these are written by the trace kernels' copy slice (anything else takes hipMemcpyAsync)
+    struct HostRange {
+        char* host;
+        size_t bytes;
+        char* mapped;
+    };
+    std::vector<HostRange> host_ranges;
     // view_params cache: the camera and frame size of the last call (this scene) and the view part
     // of LaunchParams they gave (per-sphere screen boxes: a few us of host trig per launch)
     bool view_ok = false;
@@ -424,7 +436,7 @@ struct EncTarget {
 // Launch the trace of bands (first, step) of `band_rows` rows into `out` on device d.
 int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int band_rows, int first, int step,
                 int32_t* out, int* n_bands, int fmt = RT_BANDS_INT32, int n_frames = 1, size_t frame_bytes = 0,
-                const EncTarget* enc = nullptr) {
+                const EncTarget* enc = nullptr, bool with_hand = false) {
     LaunchParams lp;
     std::memset(&lp, 0, sizeof lp);
     int rc = view_params(ctx, W, H, lp);
@@ -445,6 +457,13 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
         lp.enc_wire = enc->wire, lp.enc_stage = enc->stage;
         lp.enc_tiles_x = enc->tiles_x, lp.enc_tpf = enc->tpf, lp.enc_frame0 = enc->frame0;
     }
+    if (with_hand && d.hand.words) {  // rt_render_async: the previous frame's copy rides along
+        lp.copy_src = d.hand.src;
+        lp.copy_dst = d.hand.mapped;
+        lp.copy_words = d.hand.words;
+        lp.copy_z = 1;
+        lp.out_frame_bytes = 0;
+    }
     hipStream_t saved = d.stream;
     d.stream = stream;
     const bool timed = begin_timed(ctx, d, 0);
@@ -452,6 +471,7 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
     end_timed(d, timed);
     d.stream = saved;
     if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "trace launch failed: %s", hipGetErrorString((hipError_t)e));
+    if (with_hand) d.hand = {};  // issued
     ctx->launches++;
     for (int k = 0; k < nb; ++k) {  // pixels of rows < H in the launched bands
         const long long y0 = (long long)(first + k * step) * band_rows;
@@ -465,6 +485,31 @@ int check_ctx(rt_ctx* ctx, int W, int H) {
     if (!ctx->has_scene) return fail(ctx, RT_ERR_NO_SCENE, "rt_set_scene has not been called");
     if (W <= 0 || H <= 0 || (long long)W * H > (1LL << 31) - 1)
         return fail(ctx, RT_ERR_INVALID_ARG, "invalid frame size %dx%d", W, H);
+    return RT_OK;
+}
+
+// Device-mapped address of [host, host + bytes) when it lies inside a range registered through
+// rt_register_host and both ends allow the copy slice's 16-byte stores; else nullptr.
+int32_t* mapped_host(const rt_ctx* ctx, void* host, size_t bytes) {
+    if (((uintptr_t)host & 15) != 0) return nullptr;
+    const char* h = (const char*)host;
+    for (const rt_ctx::HostRange& r : ctx->host_ranges)
+        if (h >= r.host && bytes <= r.bytes && (size_t)(h - r.host) <= r.bytes - bytes) {
+            char* m = r.mapped + (h - r.host);
+            return ((uintptr_t)m & 15) == 0 ? (int32_t*)m : nullptr;
+        }
+    return nullptr;
+}
+
+// Issue rt_render_async's pending hand-off (the last frame's D2H) on the async stream.
+int flush_hand(rt_ctx* ctx) {
+    if (!ctx || ctx->dev.empty()) return RT_OK;
+    Device& d = ctx->dev[0];
+    if (!d.hand.words) return RT_OK;
+    DeviceGuard guard(d.id);
+    const auto h = d.hand;
+    d.hand = {};
+    HIP_TRY(ctx, hipMemcpyAsync(h.host, h.src, h.words * sizeof(int32_t), hipMemcpyDeviceToHost, d.async_stream));
     return RT_OK;
 }
 }  // namespace
@@ -555,6 +600,7 @@ int rt_create_ex(int n_gpus, int flags, rt_ctx** out_ctx) {
 
 void rt_destroy(rt_ctx* ctx) {
     if (!ctx) return;
+    (void)flush_hand(ctx);  // the last rt_render_async frame still reaches its (registered) buffer
     for (Device& d : ctx->dev) {
         DeviceGuard guard(d.id);
         (void)hipDeviceSynchronize();  // kernels on caller streams may still read our buffers
@@ -571,12 +617,7 @@ void rt_destroy(rt_ctx* ctx) {
         if (d.d_counters_diag) (void)hipFree(d.d_counters_diag);
         if (d.d_view_tab) (void)hipFree(d.d_view_tab);
         if (d.d_stage) (void)hipFree(d.d_stage);
-        for (int i = 0; i < 2; ++i) {
-            if (d.traced_ev[i]) (void)hipEventDestroy(d.traced_ev[i]);
-            if (d.copied_ev[i]) (void)hipEventDestroy(d.copied_ev[i]);
-        }
-        for (hipStream_t s : d.slot_stream)
-            if (s) (void)hipStreamDestroy(s);
+        if (d.async_stream) (void)hipStreamDestroy(d.async_stream);
         if (d.stream) (void)hipStreamDestroy(d.stream);
     }
     delete ctx;
@@ -987,11 +1028,25 @@ int rt_register_host(rt_ctx* ctx, void* host_ptr, size_t bytes) {
     if (!ctx || !host_ptr || !bytes) return fail(ctx, RT_ERR_INVALID_ARG, "rt_register_host: bad arguments");
     DeviceGuard guard(ctx->dev[0].id);
     HIP_TRY(ctx, hipHostRegister(host_ptr, bytes, hipHostRegisterDefault));
+    // the device-mapped address lets rt_render_async's trace launches write the frame into it
+    void* mapped = nullptr;
+    if (hipHostGetDevicePointer(&mapped, host_ptr, 0) == hipSuccess && mapped)
+        ctx->host_ranges.push_back({(char*)host_ptr, bytes, (char*)mapped});
+    else
+        (void)hipGetLastError();  // not mapped: rt_render_async copies with hipMemcpyAsync
     return RT_OK;
 }
 
 int rt_unregister_host(rt_ctx* ctx, void* host_ptr) {
     if (!ctx || !host_ptr) return fail(ctx, RT_ERR_INVALID_ARG, "rt_unregister_host: bad arguments");
+    // a hand-off still pending into this range is written first: nothing may touch it afterwards
+    int rc = rt_wait(ctx);
+    if (rc != RT_OK) return rc;
+    for (size_t i = 0; i < ctx->host_ranges.size(); ++i)
+        if (ctx->host_ranges[i].host == (char*)host_ptr) {
+            ctx->host_ranges.erase(ctx->host_ranges.begin() + (long)i);
+            break;
+        }
     DeviceGuard guard(ctx->dev[0].id);
     HIP_TRY(ctx, hipHostUnregister(host_ptr));
     return RT_OK;
@@ -1004,6 +1059,10 @@ int rt_render(rt_ctx* ctx, int width, int height, int32_t* pixels) {
     if (!pixels) return fail(ctx, RT_ERR_INVALID_ARG, "NULL pixels");
     const size_t frame_bytes = (size_t)width * height * sizeof(int32_t);
     Device& d0 = ctx->dev[0];
+    if (d0.hand.words) {  // rt_render_async frames first (the caller may reuse their buffers)
+        rc = rt_wait(ctx);
+        if (rc != RT_OK) return rc;
+    }
     if (!ctx->rccl_gather) {
         DeviceGuard guard(d0.id);
         rc = grow(ctx, (void**)&d0.d_frame, &d0.frame_cap, frame_bytes);
@@ -1070,12 +1129,16 @@ int rt_render(rt_ctx* ctx, int width, int height, int32_t* pixels) {
     return RT_OK;
 }
 
-// Double-buffered Tick(): frame k is traced into device buffer k % 2 on the trace stream, then
-// copied into the caller's buffer on the copy stream; frame k+1's trace overlaps frame k's D2H,
-// and the trace into a buffer waits for the copy out of it two frames earlier.  Frames complete
-// in order (one stream each for traces and copies); no host synchronisation.  (With a stream per
-// buffer, two D2H copies ran side by side and the pipeline measured 2.3k fps against the
-// synchronous Tick's 5.0k.)
+// Double-buffered Tick() on one in-order stream.  Frame k is traced into device buffer k % 2;
+// its D2H copy rides in frame k+1's launch as the copy slice (grid z = 0, dispatched ahead of the
+// trace workgroups, so the PCIe-bound copy of frame k runs under the trace of frame k+1) or is
+// issued by rt_wait.  Buffer k % 2 is traced again by launch k+2, after launch k+1 (its copy) on the
+// same stream.  The slice writes only host ranges registered through rt_register_host (their
+// device-mapped addresses); any other buffer gets hipMemcpyAsync on the same stream.
+// Measured before (tools/tick_ab.sh, profiles/r03_tick_ab.txt): a trace stream and a copy stream
+// ordered by events ran 175-195 us per frame in some processes and 350-1200 us in others -- torch's
+// own kernel-on-one-stream / D2H-on-another pattern does the same -- while one stream ran a steady
+// 195-200 us (trace, then the runtime's copy kernel, no overlap).
 int rt_render_async(rt_ctx* ctx, int width, int height, int32_t* pixels) {
     int rc = check_ctx(ctx, width, height);
     if (rc != RT_OK) return rc;
@@ -1084,32 +1147,32 @@ int rt_render_async(rt_ctx* ctx, int width, int height, int32_t* pixels) {
     Device& d = ctx->dev[0];
     DeviceGuard guard(d.id);
     const size_t frame_bytes = (size_t)width * height * sizeof(int32_t);
-    for (int i = 0; i < 2; ++i) {
-        if (!d.slot_stream[i]) HIP_TRY(ctx, hipStreamCreateWithFlags(&d.slot_stream[i], hipStreamNonBlocking));
-        if (!d.traced_ev[i]) HIP_TRY(ctx, hipEventCreateWithFlags(&d.traced_ev[i], hipEventDisableTiming));
-        if (!d.copied_ev[i]) HIP_TRY(ctx, hipEventCreateWithFlags(&d.copied_ev[i], hipEventDisableTiming));
-    }
+    if (!d.async_stream) HIP_TRY(ctx, hipStreamCreateWithFlags(&d.async_stream, hipStreamNonBlocking));
     const int slot = d.async_next;
-    hipStream_t ts = d.slot_stream[0], cs = d.slot_stream[1];
-    if (d.frames2_cap[slot] < frame_bytes) {  // (re)allocation: nothing may still use the old buffer
-        HIP_TRY(ctx, hipStreamSynchronize(ts));
-        HIP_TRY(ctx, hipStreamSynchronize(cs));
+    if (d.frames2_cap[slot] < frame_bytes) {  // (re)allocation: the pending copy may read the other
+        rc = flush_hand(ctx);                 // buffer only, but nothing may still use this one
+        if (rc != RT_OK) return rc;
+        HIP_TRY(ctx, hipStreamSynchronize(d.async_stream));
     }
     rc = grow(ctx, (void**)&d.d_frames2[slot], &d.frames2_cap[slot], frame_bytes);
     if (rc != RT_OK) return rc;
-    HIP_TRY(ctx, hipStreamWaitEvent(ts, d.copied_ev[slot], 0));  // frame k-2's copy out of this buffer
-    rc = trace_bands(ctx, d, ts, width, height, height, 0, 1, d.d_frames2[slot], nullptr);
+    static const bool nofuse = getenv("RT_ASYNC_NOFUSE") != nullptr;  // A/B probe only
+    if (nofuse) {
+        rc = flush_hand(ctx);
+        if (rc != RT_OK) return rc;
+    }
+    rc = trace_bands(ctx, d, d.async_stream, width, height, height, 0, 1, d.d_frames2[slot], nullptr, RT_BANDS_INT32,
+                     1, 0, nullptr, true);
     if (rc != RT_OK) return rc;
-    HIP_TRY(ctx, hipEventRecord(d.traced_ev[slot], ts));
-    HIP_TRY(ctx, hipStreamWaitEvent(cs, d.traced_ev[slot], 0));
-    hipStream_t saved = d.stream;
-    d.stream = cs;  // time the copy on the stream it runs on
-    const bool ctimed = begin_timed(ctx, d, 1);
-    hipError_t e = hipMemcpyAsync(pixels, d.d_frames2[slot], frame_bytes, hipMemcpyDeviceToHost, cs);
-    end_timed(d, ctimed);
-    d.stream = saved;
-    if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "rt_render_async: %s", hipGetErrorString(e));
-    HIP_TRY(ctx, hipEventRecord(d.copied_ev[slot], cs));
+    int32_t* mapped = nofuse ? nullptr : mapped_host(ctx, pixels, frame_bytes);
+    if (mapped) {
+        d.hand.host = pixels;
+        d.hand.mapped = mapped;
+        d.hand.src = d.d_frames2[slot];
+        d.hand.words = (size_t)width * height;
+    } else {
+        HIP_TRY(ctx, hipMemcpyAsync(pixels, d.d_frames2[slot], frame_bytes, hipMemcpyDeviceToHost, d.async_stream));
+    }
     d.async_next = slot ^ 1;
     ctx->frames++;
     ctx->pixels += (uint64_t)width * (uint64_t)height;
@@ -1118,11 +1181,12 @@ int rt_render_async(rt_ctx* ctx, int width, int height, int32_t* pixels) {
 
 int rt_wait(rt_ctx* ctx) {
     if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "NULL context");
+    int rc = flush_hand(ctx);
+    if (rc != RT_OK) return rc;
     for (Device& d : ctx->dev) {
         DeviceGuard guard(d.id);
         HIP_TRY(ctx, hipStreamSynchronize(d.stream));
-        for (hipStream_t st : d.slot_stream)
-            if (st) HIP_TRY(ctx, hipStreamSynchronize(st));
+        if (d.async_stream) HIP_TRY(ctx, hipStreamSynchronize(d.async_stream));
     }
     return RT_OK;
 }

@@ -131,6 +131,14 @@ struct LaunchParams {
     uint32_t* enc_stage;
     int enc_tiles_x, enc_tpf, enc_frame0;
     unsigned long long* counters;  // COUNTER_SLOTS x COUNTER_STRIDE (CNT_*)
+    // rt_render_async's fused hand-off: with copy_z = 1 the launch has one more grid z-slice,
+    // z = 0, whose workgroups copy copy_words int32 from copy_src (the previous frame, device) to
+    // copy_dst (its caller's registered host buffer, device-mapped address); the launch's one
+    // frame is z = 1 (out_frame_bytes 0).  copy_z = 0: no slice.
+    const int32_t* copy_src;
+    int32_t* copy_dst;
+    unsigned long long copy_words;
+    int copy_z;
     int prim_const;                // 1: pc[0..S) and pbox[0..S) valid (S <= MAX_PRIM_CONST)
     PrimConst pc[MAX_PRIM_CONST];
     PrimBox pbox[MAX_PRIM_CONST];

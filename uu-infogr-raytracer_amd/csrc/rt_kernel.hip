@@ -201,9 +201,25 @@ __device__ __forceinline__ uint32_t shift_channel(float c) {
 // row y (format 2), or packed 24-bit (B, G, R bytes; the top byte of the int32 is always 0)
 // for band sets shipped to rank 0 -- a quarter fewer bytes over xGMI (format 1).
 // Format 2 (RT_BANDS_FRAME): the rank's bands straight into the row-major frame (row y).
+// The copy slice (z = 0) of rt_render_async's launch: the previous frame, device -> the caller's
+// registered host buffer, 16 bytes per lane (both ends 16-byte aligned, checked on the host), grid-
+// strided over the slice's workgroups.  Dispatched before the trace workgroups of the same launch,
+// so the PCIe-bound copy of frame k-1 runs under the trace of frame k on one in-order stream.
+__device__ __forceinline__ void copy_slice(const LaunchParams& p) {
+    const size_t lane = threadIdx.x & 63;
+    const size_t nwg = (size_t)gridDim.x * gridDim.y;
+    const size_t wg = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    const unsigned long long n = p.copy_words, n4 = n / 4;
+    const int4* __restrict__ s4 = (const int4*)p.copy_src;
+    int4* __restrict__ d4 = (int4*)p.copy_dst;
+    for (size_t i = wg * 64 + lane; i < n4; i += nwg * 64) d4[i] = s4[i];
+    if (wg == 0 && lane < n - n4 * 4) p.copy_dst[n4 * 4 + lane] = p.copy_src[n4 * 4 + lane];
+}
+
 __device__ __forceinline__ void store_pixel(const LaunchParams& p, int r, int y, int x, uint32_t px32) {
     const size_t i = (size_t)(p.out_fmt == 2 ? y : r) * (size_t)p.W + (size_t)x;
-    unsigned char* base = (unsigned char*)p.out + (size_t)blockIdx.z * p.out_frame_bytes;  // batch frame z
+    // batch frame z (a launch with the copy slice has one frame and out_frame_bytes 0)
+    unsigned char* base = (unsigned char*)p.out + (size_t)blockIdx.z * p.out_frame_bytes;
     if (p.out_fmt != 1) {
         ((int32_t*)base)[i] = (int32_t)px32;
     } else {
@@ -409,7 +425,7 @@ struct Tally<true, SMAX> {
 template <bool ST, int SM>
 __device__ __forceinline__ void add_counters(const LaunchParams& p, int lane, unsigned n_refl, unsigned n_shadow,
                                              const Tally<ST, SM>& tl) {
-    if (blockIdx.z != 0) return;  // wave-uniform
+    if (blockIdx.z != (unsigned)p.copy_z) return;  // wave-uniform: the first frame (behind a copy slice)
     const unsigned long long nf = p.n_frames > 1 ? (unsigned long long)p.n_frames : 1ull;
     const unsigned b = wave_count(n_refl), c = wave_count(n_shadow);
     const unsigned slot = (blockIdx.y * gridDim.x + blockIdx.x) % COUNTER_SLOTS;
@@ -775,6 +791,10 @@ __global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p
     constexpr int LDS_LEVELS = StackFor<K>::lds_levels;  // LdsStack slots, else unused
     __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
     __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * WG_THREADS : 1];
+    if (blockIdx.z < (unsigned)p.copy_z) {  // wave-uniform: the fused hand-off's copy slice
+        copy_slice(p);
+        return;
+    }
     Tally<STATS, SMAX> tl;
     const unsigned cnt = trace_tile_direct<K, GPOW, TILES>(p, blockIdx.x, stk_lv, stk_dv, tl);
     add_counters<STATS>(p, threadIdx.x & 63, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
@@ -1278,6 +1298,10 @@ __device__ __forceinline__ void bundle_kernel_body(const LaunchParams& p) {
     constexpr int LDS_LEVELS = StackFor<K>::lds_levels;  // LdsStack slots, else unused
     __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
     __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * WG_THREADS : 1];
+    if (blockIdx.z < (unsigned)p.copy_z) {  // wave-uniform: the fused hand-off's copy slice
+        copy_slice(p);
+        return;
+    }
     Tally<STATS> tl;
     const unsigned cnt = trace_tile_bundle<K, GPOW, TILES>(p, blockIdx.x, stk_lv, stk_dv, tl);
     add_counters<STATS>(p, threadIdx.x & 63, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
@@ -1432,7 +1456,7 @@ static void launch_variant(const LaunchParams& p, bool bundle, dim3 grid, dim3 b
 int launch_trace(const LaunchParams& p, bool generic_pow, bool stats, void* stream) {
     if (p.local_rows <= 0 || p.W <= 0) return (int)hipSuccess;
     const dim3 grid((unsigned)((p.W + TILE_W - 1) / TILE_W), (unsigned)((p.local_rows + TILE_H - 1) / TILE_H),
-                    (unsigned)(p.n_frames > 1 ? p.n_frames : 1));
+                    (unsigned)(p.n_frames > 1 ? p.n_frames : 1) + (unsigned)p.copy_z);
     const dim3 block(WG_THREADS);
     hipStream_t s = (hipStream_t)stream;
     // bundle culling pays for its per-wave bounds only with enough spheres (A/B: +15 % at
