@@ -52,6 +52,10 @@ def parse(argv=None):
                     help="N=1: keep warming up (untimed, whole launches) until this much wall time has passed -- "
                          "the GPU needs ~10-50 ms of load to reach its steady clock; reported as warmup_effective")
     ap.add_argument("--config", default="C2")
+    ap.add_argument("--also-dist", default="C5",
+                    help="N>1: comma list of further configs run through the same band pipeline after --config and "
+                         "reported under 'also' (default C5: 7680x4320, the config BASELINE names for the 1/2/4/8-GPU "
+                         "scaling curve); '' = none")
     ap.add_argument("--also", default="C3",
                     help="N=1: comma list of further configs measured in the same run and reported under 'also' "
                          "(default C3, the north-star config: depth 4, 2 lights); '' = none")
@@ -422,9 +426,26 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=world)
     else:
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local))
-    sc = scenes.config(args.config)
-    if args.size:
-        w_, h_ = map(int, args.size.lower().split("x"))
+    out = dist_leg(args, args.config, rank, world, local, torch, dist, Context, abi, scenes, size=args.size)
+    # further configs through the same pipeline (default C5: 7680x4320, the configuration BASELINE
+    # names for the 1/2/4/8-GPU scaling curve), each with its own value / ms_per_step / n_gpus
+    also = [c for c in (x.strip() for x in args.also_dist.split(",")) if c and c.upper() != args.config.upper()]
+    for name in also:
+        o2 = dist_leg(args, name, rank, world, local, torch, dist, Context, abi, scenes)
+        if rank == 0:
+            out.setdefault("also", {})[o2["config"]["workload"].split(":")[0]] = {
+                k: o2[k] for k in ("value", "unit", "n_gpus", "steps", "ms_per_step", "fps", "config", "roofline")}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    dist.destroy_process_group()
+
+
+def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, scenes, size=""):
+    """One N > 1 measurement of `config_name` through the band pipeline (rank 0 returns the
+    line's dict, the other ranks None).  Every rank runs every leg, so the collectives match."""
+    sc = scenes.config(config_name)
+    if size:  # probe runs only (--size): the config's scene at another frame size
+        w_, h_ = map(int, size.lower().split("x"))
         sc = sc.resized(w_, h_, f"{sc.name}@{w_}x{h_}")
     W, H = sc.width, sc.height
     ctx = Context(1)
@@ -753,10 +774,8 @@ def main():
             out["config"]["gather_redone_batches"] = gather_info["redone"]
         if args.verify:
             out["verified_frames"] = verified
-        print(json.dumps(out), flush=True)
     ctx.close()
-    if distributed:
-        dist.destroy_process_group()
+    return out if rank == 0 else None
 
 
 def verify_rings(ctx, tg, W, H, steps, torch):

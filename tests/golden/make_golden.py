@@ -88,6 +88,19 @@ def pin(chunk_rows: int = 256):
         print(line, flush=True)
         lines.append(line)
         assert ok, line
+    # the independent numpy float32 emulation (all-hit, written from the C#) on C4's scene (= C5's)
+    # at a mid size, beside both drivers
+    sc = scenes.config("C4").resized(384, 216)
+    t0 = time.time()
+    emu = emu_f32.Emu(sc).render()
+    near, _ = pyoracle.render(sc, pyoracle.MODE_NEAREST, nthreads)
+    ref, _ = pyoracle.render(sc, pyoracle.MODE_REFERENCE, nthreads)
+    ok = np.array_equal(emu, near) and np.array_equal(emu, ref)
+    line = (f"C4/C5 scene   384x216 numpy emulation {crc(emu)} nearest {crc(near)} all-hit {crc(ref)} "
+            f"{'OK' if ok else 'FAIL'} ({time.time() - t0:.1f} s)")
+    print(line, flush=True)
+    lines.append(line)
+    assert ok, line
     with open(os.path.join(HERE, "pin_allhit.log"), "w") as f:
         f.write("\n".join(lines) + "\n")
 

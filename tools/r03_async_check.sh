@@ -12,3 +12,5 @@ timeout -k 10 120 python3 -u tools/tick_trace.py > $O/tick_fused.txt 2>&1
 RT_ASYNC_NOFUSE=1 timeout -k 10 120 python3 -u tools/tick_trace.py > $O/tick_nofuse.txt 2>&1
 timeout -k 10 120 python3 -u tools/tick_trace.py > $O/tick_fused2.txt 2>&1
 timeout -k 10 300 python3 -u bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err
+# the N > 1 pipeline in one process (RCCL world of 1): C2, then C5 through the also-dist leg
+timeout -k 10 300 python3 -u bench.py --dist-path --rank0-codec --steps 20 --warmup 5 --verify > $O/distpath.json 2> $O/distpath.err

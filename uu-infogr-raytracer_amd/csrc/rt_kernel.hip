@@ -202,17 +202,31 @@ __device__ __forceinline__ uint32_t shift_channel(float c) {
 // for band sets shipped to rank 0 -- a quarter fewer bytes over xGMI (format 1).
 // Format 2 (RT_BANDS_FRAME): the rank's bands straight into the row-major frame (row y).
 // The copy slice (z = 0) of rt_render_async's launch: the previous frame, device -> the caller's
-// registered host buffer, 16 bytes per lane (both ends 16-byte aligned, checked on the host), grid-
-// strided over the slice's workgroups.  Dispatched before the trace workgroups of the same launch,
-// so the PCIe-bound copy of frame k-1 runs under the trace of frame k on one in-order stream.
+// registered host buffer, 16 bytes per lane (both ends 16-byte aligned, checked on the host).
+// Dispatched before the trace workgroups of the same launch, so the PCIe-bound copy of frame k-1
+// runs under the trace of frame k on one in-order stream.  Only the slice's first COPY_WAVES
+// workgroups copy (grid-strided, 4 loads in flight per lane), the others exit at once: a wave
+// holds its slot until its host stores are acknowledged, and a slice of one-store waves (8,100 at
+// 1080p) held nearly every wave slot of the chip until PCIe had drained them, so the trace waited.
+constexpr unsigned COPY_WAVES = 512;
 __device__ __forceinline__ void copy_slice(const LaunchParams& p) {
     const size_t lane = threadIdx.x & 63;
-    const size_t nwg = (size_t)gridDim.x * gridDim.y;
+    const size_t nwg = min((size_t)gridDim.x * gridDim.y, (size_t)COPY_WAVES);
     const size_t wg = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    if (wg >= nwg) return;
     const unsigned long long n = p.copy_words, n4 = n / 4;
     const int4* __restrict__ s4 = (const int4*)p.copy_src;
     int4* __restrict__ d4 = (int4*)p.copy_dst;
-    for (size_t i = wg * 64 + lane; i < n4; i += nwg * 64) d4[i] = s4[i];
+    const size_t step = nwg * 64;
+    size_t i = wg * 64 + lane;
+    for (; i + 3 * step < n4; i += 4 * step) {
+        const int4 a = s4[i], b = s4[i + step], c = s4[i + 2 * step], d = s4[i + 3 * step];
+        d4[i] = a;
+        d4[i + step] = b;
+        d4[i + 2 * step] = c;
+        d4[i + 3 * step] = d;
+    }
+    for (; i < n4; i += step) d4[i] = s4[i];
     if (wg == 0 && lane < n - n4 * 4) p.copy_dst[n4 * 4 + lane] = p.copy_src[n4 * 4 + lane];
 }
 
