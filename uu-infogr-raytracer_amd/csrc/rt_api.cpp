@@ -1328,6 +1328,7 @@ int rt_count_work(rt_ctx* ctx, int width, int height, rt_work* out) {
     lp.out = d.d_frame;
     lp.out_fmt = RT_BANDS_INT32;
     lp.n_frames = 1;
+    if (const char* sel = getenv("RT_DIAG_SEL")) lp.enc_frame0 = atoi(sel);  // RT_SHADOW_CAT diagnostic builds only
     int e = launch_trace(lp, ctx->layout.generic_pow, true, d.stream);
     if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "rt_count_work launch: %s", hipGetErrorString((hipError_t)e));
     std::vector<unsigned long long> h(COUNTER_WORDS);

@@ -410,6 +410,14 @@ constexpr unsigned CNT_REFL_MASK = 0xFFu;
 #ifndef RT_SLOT_TALLY
 #define RT_SLOT_TALLY 0
 #endif
+// RT_SHADOW_CAT=1 (diagnostic builds, tools/shadow_slots.py): sphere_tests_run counts only the
+// bundle kernel's shadow-test lane slots of one category, chosen at run time by rt_count_work's
+// selector (RT_DIAG_SEL = 16 * category + level + 1, level -1 = every fold level): category 1
+// useful (needed, not yet blocked), 2 needed but already blocked, 3 diffuse but not needed,
+// 4 active record, not diffuse, 5 no record at this level.
+#ifndef RT_SHADOW_CAT
+#define RT_SHADOW_CAT 0
+#endif
 template <bool ON, int SMAX = 0>
 struct Tally {
     static constexpr int smax = SMAX;
@@ -417,17 +425,31 @@ struct Tally {
     __device__ __forceinline__ void shadow_sphere(bool) {}
     __device__ __forceinline__ void plane(bool) {}
     __device__ __forceinline__ void shadow(bool) {}
+    __device__ __forceinline__ void init(const LaunchParams&) {}
+    __device__ __forceinline__ void set_level(int) {}
+    __device__ __forceinline__ void shadow_cat(int, unsigned) {}
 };
 template <int SMAX>
 struct Tally<true, SMAX> {
     static constexpr int smax = SMAX;
     unsigned s = 0, pl = 0, sh = 0;
+    int lvl = 0, sel_cat = 0, sel_lvl = -1;
     // RT_SLOT_TALLY (diagnostic builds, tools/slot_probe.py): lane slots of the exact tests,
     // useful or not -- 1: every sphere test, 2: the nearest-hit tests only
-    __device__ __forceinline__ void sphere(bool c) { s += (RT_SLOT_TALLY || c) ? 1u : 0u; }
-    __device__ __forceinline__ void shadow_sphere(bool c) { s += (RT_SLOT_TALLY == 1 || c) ? 1u : 0u; }
+    __device__ __forceinline__ void sphere(bool c) { s += (!RT_SHADOW_CAT && (RT_SLOT_TALLY || c)) ? 1u : 0u; }
+    __device__ __forceinline__ void shadow_sphere(bool c) {
+        s += (!RT_SHADOW_CAT && (RT_SLOT_TALLY == 1 || c)) ? 1u : 0u;
+    }
     __device__ __forceinline__ void plane(bool c) { pl += c ? 1u : 0u; }
     __device__ __forceinline__ void shadow(bool c) { sh += c ? 1u : 0u; }
+    __device__ __forceinline__ void init(const LaunchParams& p) {
+        sel_cat = p.enc_frame0 / 16;
+        sel_lvl = p.enc_frame0 % 16 - 1;
+    }
+    __device__ __forceinline__ void set_level(int l) { lvl = l; }
+    __device__ __forceinline__ void shadow_cat(int cat, unsigned n) {
+        s += (RT_SHADOW_CAT && cat + 1 == sel_cat && (sel_lvl < 0 || lvl == sel_lvl)) ? n : 0u;
+    }
 };
 
 // Work counters of one wave (converged call): ballot/popcount sums, lane 0 adds the wave's
@@ -1165,6 +1187,7 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
                         const int i1 = two ? base + (int)__builtin_ctzll(mk64) : i0;
                         if (two) mk64 &= mk64 - 1;
                         const DevSphere s0 = p.sph[i0], s1 = p.sph[i1];
+                        tl.shadow_cat(need ? (blocked ? 1 : 0) : (diff ? 2 : (act ? 3 : 4)), 2u);
                         tl.shadow_sphere(!blocked);
                         const bool h0 = shadow_blocked<false, true>(hs, l, l_ok, s0);
                         tl.shadow_sphere(two && !blocked && !h0);
@@ -1216,6 +1239,7 @@ __device__ __forceinline__ f3 fold_converged(const LaunchParams& p, STK& stk, f3
         }
         const int code = __float_as_int(rb.w);
         const bool is_s = code >= 0;
+        tl.set_level(level);
         col = shade_bundle<GPOW>(p, act, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z), ra.w,
                                  col, cnt, tl);
     }
@@ -1317,6 +1341,7 @@ __device__ __forceinline__ void bundle_kernel_body(const LaunchParams& p) {
         return;
     }
     Tally<STATS> tl;
+    tl.init(p);
     const unsigned cnt = trace_tile_bundle<K, GPOW, TILES>(p, blockIdx.x, stk_lv, stk_dv, tl);
     add_counters<STATS>(p, threadIdx.x & 63, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
 }
