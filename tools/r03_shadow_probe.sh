@@ -6,4 +6,4 @@ R=${GRAFT_REPO_ROOT:-/root/repo}
 O=$R/gpurun_out/r03s
 mkdir -p $O
 cd $R
-timeout -k 10 600 python3 -u tools/shadow_slots.py --configs C4 C5 > $O/shadow_slots.txt 2>&1
+timeout -k 10 600 python3 -u tools/shadow_slots.py --configs C4 > $O/shadow_slots.txt 2>&1

@@ -42,6 +42,11 @@ def main():
             print(f"  {CATS[c - 1]:22s}" + " ".join(f"{v:13,d}" for v in tab[c]) + f" {sum(tab[c]):13,d}", flush=True)
         lvl_tot = [sum(tab[c][lv] for c in tab) for lv in range(a.levels)]
         print(f"  {'all':22s}" + " ".join(f"{v:13,d}" for v in lvl_tot), flush=True)
+        # overlap of the lights' candidate sets (per wave and shaded level): sum over lights vs union
+        per = [count(a.lib, n, 16 * 6 + lv + 1) for lv in range(a.levels)]
+        uni = [count(a.lib, n, 16 * 7 + lv + 1) for lv in range(a.levels)]
+        print(f"  {'cands, sum of lights':22s}" + " ".join(f"{v:13,d}" for v in per) + f" {sum(per):13,d}", flush=True)
+        print(f"  {'cands, union':22s}" + " ".join(f"{v:13,d}" for v in uni) + f" {sum(uni):13,d}", flush=True)
 
 
 if __name__ == "__main__":

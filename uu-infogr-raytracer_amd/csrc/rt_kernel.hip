@@ -418,6 +418,7 @@ constexpr unsigned CNT_REFL_MASK = 0xFFu;
 #ifndef RT_SHADOW_CAT
 #define RT_SHADOW_CAT 0
 #endif
+
 template <bool ON, int SMAX = 0>
 struct Tally {
     static constexpr int smax = SMAX;
@@ -428,6 +429,7 @@ struct Tally {
     __device__ __forceinline__ void init(const LaunchParams&) {}
     __device__ __forceinline__ void set_level(int) {}
     __device__ __forceinline__ void shadow_cat(int, unsigned) {}
+    __device__ __forceinline__ void shadow_masks(int, unsigned long long) {}
 };
 template <int SMAX>
 struct Tally<true, SMAX> {
@@ -449,6 +451,12 @@ struct Tally<true, SMAX> {
     __device__ __forceinline__ void set_level(int l) { lvl = l; }
     __device__ __forceinline__ void shadow_cat(int cat, unsigned n) {
         s += (RT_SHADOW_CAT && cat + 1 == sel_cat && (sel_lvl < 0 || lvl == sel_lvl)) ? n : 0u;
+    }
+    // categories 6 / 7 (lane 0 only): candidates per light's shadow pass / of the union of a shaded
+    // level's lights -- how far the lights' candidate sets overlap
+    __device__ __forceinline__ void shadow_masks(int cat, unsigned long long m) {
+        if (RT_SHADOW_CAT && cat + 1 == sel_cat && (sel_lvl < 0 || lvl == sel_lvl) && (threadIdx.x & 63) == 0)
+            s += (unsigned)__builtin_popcountll(m);
     }
 };
 
@@ -1122,6 +1130,66 @@ __device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d,
     return Hit{0.0f, HIT_NONE};
 }
 
+// Merged shadow pass of one shaded level (bundle kernel, S <= 64 spheres, L <= SHADOW_MERGE_L
+// lights): every light's shadow rays of the wave in ONE wave-uniform loop over the union of the
+// lights' candidate sets (they share the level's ShadowSphere bound, and the sets overlap: on C4
+// the union holds ~1/3 of the per-light sum, profiles/r03_shadow_slots.txt).  Per candidate sphere
+// oc = hp - c and c = oc.oc - r^2 are shared by the lights; b, disc and the root test are per light,
+// for the lights whose candidate set holds the sphere and which still have a pending lane (both
+// wave-uniform).  Operations and their order are exactly shadow_blocked's (:613-642 with
+// IntersectShadowLight's :574-578), so every outcome is the same bit.  Returns the lane's blocked
+// bits (bit li).  `want` (bit li): the lane's ray toward light li must be resolved -- a superset of
+// the shading's `need` (shade_bundle), so every needed outcome is computed.
+constexpr int SHADOW_MERGE_L = 4;
+template <typename T>
+__device__ __forceinline__ unsigned shadow_merged(const LaunchParams& p, const ShadowSphere& SS, f3 hp, unsigned want,
+                                                  bool diff, bool act, T& tl) {
+    // candidate sets as one register: lane i holds bit li when sphere i is a candidate for light li
+    const int lane = threadIdx.x & 63;
+    unsigned memb = 0;
+    for (int li = 0; li < p.L; ++li)
+        if (__builtin_amdgcn_ballot_w64((want >> li) & 1u) != 0) {
+            const unsigned long long cm = shadow_sphere_cull(p, SS, p.li[li], li, 0, p.S);
+            memb |= ((cm >> lane) & 1ull) ? (1u << li) : 0u;
+        }
+    unsigned long long U = __builtin_amdgcn_ballot_w64(memb != 0u);
+    unsigned blk = 0;
+    while (U) {
+        const int i = (int)__builtin_ctzll(U);
+        U &= U - 1;
+        const unsigned mi = (unsigned)__builtin_amdgcn_readlane((int)memb, i);  // lights with sphere i
+        const DevSphere sp = p.sph[i];
+        const f3 oc = sub(hp, mk(sp.cx, sp.cy, sp.cz));  // shared by the lights (shadow_blocked's oc, c)
+        const float c = dot(oc, oc) - sp.r2;
+#pragma unroll
+        for (int li = 0; li < SHADOW_MERGE_L; ++li) {
+            if (((mi >> li) & 1u) == 0) continue;  // wave-uniform (li < p.L)
+            const bool pending = ((want & ~blk) >> li) & 1u;
+            if (__builtin_amdgcn_ballot_w64(pending) == 0) continue;  // wave-uniform
+            tl.shadow_cat(pending ? 0 : (((want >> li) & 1u) ? 1 : (diff ? 2 : (act ? 3 : 4))), 1u);
+            tl.shadow_sphere(pending);
+            const DevLight& l = p.li[li];
+            const float b = 2.0f * dot(oc, mk(l.px, l.py, l.pz));
+            const float disc = b * b - l.a4 * c;
+            bool hit = false;
+            if (l.a2 > 0.0f && l.a2 < __builtin_inff()) {  // wave-uniform (shadow_blocked<.., THRESH>)
+                if (__builtin_amdgcn_ballot_w64(sphere_candidate(b, disc)) != 0) {
+                    const float sq = cr_sqrt(disc);
+                    hit = -b - sq >= l.sh_t;
+                }
+            } else if (disc >= 0.0f) {
+                const float sq = __builtin_sqrtf(disc);
+                const float t2 = (-b + sq) / l.a2;
+                const float t1 = (-b - sq) / l.a2;
+                hit = nmin(nmax0(t1 - 0.001f), nmax0(t2 - 0.001f)) > 0.0f;
+            }
+            blk |= (pending && hit) ? (1u << li) : 0u;
+        }
+        if (__builtin_amdgcn_ballot_w64((want & ~blk) != 0u) == 0) break;  // every wanted ray resolved
+    }
+    return blk;
+}
+
 // Shading of one shaded hit per active lane (TraceSphere :847-873 / TracePlane :736-778),
 // converged call: the colour is accumulated in the reference's order -- mirror term (from
 // the deeper segment `sec`), then each light in order, then ambient.  Inactive lanes
@@ -1133,6 +1201,19 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
     // idle lanes (act false) carry a copy of an active lane's record: same branches, result dropped
     const DevMaterial& m = p.mat[is_sphere ? prim : p.S + prim];
     const uint32_t flags = m.flags;
+    const bool diff = act && (flags & MAT_DIFFUSE) != 0;
+    // S <= 64 and L <= SHADOW_MERGE_L: every light's shadow rays of the level in one merged pass,
+    // first -- before the shading's own state is live.  Every diffuse lane's ray toward every light
+    // is resolved (a superset of the shading's `need`); a cheap back-facing filter that skipped
+    // some of them measured slower (C4 420 vs 401 us: its arithmetic on every lane of every level
+    // cost more than the tests it saved, profiles/ab/r03_shadow_merged.txt).
+    const bool merged = p.S <= 64 && p.L >= 1 && p.L <= SHADOW_MERGE_L && __builtin_amdgcn_ballot_w64(diff) != 0;
+    unsigned blk = 0;
+    if (merged) {
+        const unsigned want = diff ? (1u << p.L) - 1u : 0u;
+        for (int li = 0; li < p.L; ++li) tl.shadow(diff);  // (diagnostic tally of the rays resolved)
+        blk = shadow_merged(p, make_shadow_sphere(hp, diff), hp, want, diff, act, tl);
+    }
     f3 normal;
     float tile = 1.0f;
     if (is_sphere) {
@@ -1148,13 +1229,14 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
     }
     f3 col = mk(0.0f, 0.0f, 0.0f);
     if (flags & MAT_MIRROR) col = add(col, mul(sec, mk(m.km[0], m.km[1], m.km[2])));
-    const bool diff = act && (flags & MAT_DIFFUSE) != 0;
     if (__builtin_amdgcn_ballot_w64(diff) != 0) {
         const f3 view = normalize(d);  // ShapePhongShading :668 (not negated)
         // sphere: (1 / t) * t (:866);  plane: (float)(1 / Math.Pow(t, 2)) (:754), exact as 1/(t*t) in f64
         const float att = is_sphere ? cr_rcp(t) * t : (float)(1.0 / ((double)t * (double)t));
         const f3 kd = mk(m.kd[0], m.kd[1], m.kd[2]);
-        const ShadowSphere SS = make_shadow_sphere(hp, diff);  // one bound for every light's shadow rays
+        ShadowSphere SS{};
+        if (!merged) SS = make_shadow_sphere(hp, diff);  // one bound for every light's shadow rays
+        unsigned long long umask = 0;  // (diagnostic builds: the union of the lights' candidates)
         for (int li = 0; li < p.L; ++li) {
             const DevLight& l = p.li[li];
             const f3 lp = mk(l.px, l.py, l.pz);
@@ -1170,13 +1252,15 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
             }
             ph = add(ph, spec);
             const bool need = diff && shadow_matters(ph, l.intensity, att);
-            bool blocked = !need;
-            if (__builtin_amdgcn_ballot_w64(need) != 0) {  // some lane's pixel depends on this test
+            bool blocked = merged ? ((blk >> li) & 1u) != 0 : !need;
+            if (!merged && __builtin_amdgcn_ballot_w64(need) != 0) {  // some lane's pixel depends on this test
                 tl.shadow(need);
                 const f3 hs = need ? hp : SS.O;  // idle lanes mirror a shading lane (results ignored)
                 for (int base = 0; base < p.S; base += 64) {
                     const int n = min(64, p.S - base);
                     unsigned long long mk64 = shadow_sphere_cull(p, SS, l, li, base, n);
+                    tl.shadow_masks(5, mk64);
+                    umask |= mk64;
                     // candidates two at a time: independent tests (ILP across the sqrt chains),
                     // one pair of sphere loads and one exit ballot per pair; an odd last
                     // candidate is tested twice (the OR is unchanged)
@@ -1208,6 +1292,7 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
             if (diff) col = add(col, term);
         }
         if (diff) *n_shadow += (unsigned)p.L << CNT_SHADOW_SHIFT;
+        tl.shadow_masks(6, umask);
     }
     col = add(col, mk(m.amb[0], m.amb[1], m.amb[2]));
     return act ? col : sec;
@@ -1253,7 +1338,7 @@ __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int
                                                       T& tl) {
     const int lane = threadIdx.x & 63;
     const TilePixel tpx = tile_pixel(p, tile_x * TILE_W + (lane & 7), blockIdx.y * TILE_H + (lane >> 3));
-    const int x = tpx.x, r = tpx.r, y = tpx.y;
+    const int x = tpx.x, y = tpx.y;
     const bool valid = tpx.valid;
 
     unsigned cnt = 0;  // packed: reflected segments (bits 0-7) | shadow rays << CNT_SHADOW_SHIFT
@@ -1321,7 +1406,14 @@ __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int
     const f3 col = fold_converged<GPOW>(p, stk, leaf, &cnt, tl);
     const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
     if constexpr (TILES) encode_tile_fused(p, px32, valid);
-    else if (valid) store_pixel(p, r, y, x, px32);
+    else {
+        // the pixel's coordinates again, from the lane id (mbcnt) and the block id: cheaper than
+        // keeping x, r, y and `valid` live through the walk and the fold (64-VGPR cap: they were
+        // the values spilled to scratch once the merged shadow pass raised the peak)
+        const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+        const TilePixel q = tile_pixel(p, tile_x * TILE_W + (ln & 7), blockIdx.y * TILE_H + (ln >> 3));
+        if (q.valid) store_pixel(p, q.r, q.y, q.x, px32);
+    }
     return cnt;
 }
 
