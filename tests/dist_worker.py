@@ -243,6 +243,9 @@ def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batc
         read_out(frames)
         if speculate and speculate < 1 and spec_after_drain:  # (only a batch that finds the pipeline
             assert g.redone > 0, "a margin below 1 must force a gather at the real size"  # empty guesses)
+            # a redone batch was decoded twice and the second decode stands
+            assert sum(1 for n in g.decodes_of.values() if n == 2) == g.redone, g.decodes_of
+        assert not g.provisional, f"batches left provisional after drain: {g.provisional}"
         if rank == 0:
             bad = [k for k in range(frames)
                    if k not in got or not np.array_equal(got[k], pyoracle.render(scene_for(k), pyoracle.MODE_NEAREST, 2)[0])]

@@ -156,6 +156,31 @@ def test_fused_encoder_rejects_bad_arguments(gpu_ctx):
         gpu_ctx.render_bands_tiles(64, 64, 8, 0, 1, 0, 1, 1, wire.data_ptr() + 4)
 
 
+def test_finish_wire_only_finishes_the_staged_batch(gpu_ctx):
+    """rt_finish_wire compacts the codec scratch of the batch rt_render_bands_tiles staged
+    last -- another geometry, rank, wire, more frames than the batch, or a batch whose scratch an
+    rt_encode_bands has reused since, is an error instead of a wire made of stale scratch."""
+    import torch
+    from raytracer_hip import RayTracerError
+    gpu_ctx.set_scene(scenes.config("C2").resized(96, 64))
+    wire = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
+    other = torch.zeros(1 << 20, dtype=torch.uint8, device="cuda")
+    size_t = torch.zeros(1, dtype=torch.int64, device="cuda")
+    gpu_ctx.render_bands_tiles(96, 64, 8, 1, 2, 0, 2, 3, wire.data_ptr())
+    for args in [(96, 64, 8, 0, 2, 2, wire), (96, 64, 8, 1, 3, 2, wire), (96, 48, 8, 1, 2, 2, wire),
+                 (96, 64, 4, 1, 2, 2, wire), (96, 64, 8, 1, 2, 2, other), (96, 64, 8, 1, 2, 4, wire)]:
+        with pytest.raises(RayTracerError):
+            gpu_ctx.finish_wire(*args[:6], args[6].data_ptr(), size_t.data_ptr())
+    gpu_ctx.finish_wire(96, 64, 8, 1, 2, 2, wire.data_ptr(), size_t.data_ptr())  # the staged batch itself
+    torch.cuda.synchronize()
+    assert int(size_t.item()) > 0
+    bands = torch.zeros(96 * 64, dtype=torch.int32, device="cuda")
+    gpu_ctx.encode_bands(96, 64, 8, 1, 2, bands.data_ptr(), 96 * 32, 1, other.data_ptr(), size_t.data_ptr())
+    with pytest.raises(RayTracerError):  # the scratch now holds that encode's segments
+        gpu_ctx.finish_wire(96, 64, 8, 1, 2, 2, wire.data_ptr(), size_t.data_ptr())
+    torch.cuda.synchronize()
+
+
 def test_encode_rejects_bad_arguments(gpu_ctx):
     import torch
     from raytracer_hip import RayTracerError

@@ -84,6 +84,13 @@ struct Device {
     size_t gather_cap = 0;
     void* d_stage = nullptr;  // rt_encode_bands scratch (encodes on one context are stream-ordered)
     size_t stage_cap = 0;
+    // the batch whose tiles rt_render_bands_tiles last staged in d_stage (rt_finish_wire finishes only
+    // that one; rt_encode_bands reuses the scratch and clears it)
+    struct {
+        bool valid = false;
+        int W = 0, H = 0, band_rows = 0, rank = 0, world = 0, batch_frames = 0;
+        const void* wire = nullptr;
+    } staged;
     int32_t* d_frames2[2] = {nullptr, nullptr};  // rt_render_async double buffer
     size_t frames2_cap[2] = {0, 0};
     // rt_render_async: one in-order stream; frame k's D2H rides in frame k+1's launch (the copy
@@ -960,6 +967,7 @@ int rt_encode_bands(rt_ctx* ctx, int width, int height, int band_rows, int rank,
     DeviceGuard guard(d.id);
     const int rc = ensure_stage(ctx, d, g);
     if (rc != RT_OK) return rc;
+    d.staged.valid = false;  // the scratch now holds this encode's segments
     int e = launch_encode_bands(d_bands, (unsigned char*)d_wire, g, d_wire_bytes, d.d_stage, hip_stream);
     if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "encode launch: %s", hipGetErrorString((hipError_t)e));
     return RT_OK;
@@ -983,7 +991,11 @@ int rt_render_bands_tiles(rt_ctx* ctx, int width, int height, int band_rows, int
     int nb = 0;
     rc = trace_bands(ctx, d, (hipStream_t)hip_stream, width, height, band_rows, rank, world, (int32_t*)d_wire, &nb,
                      RT_BANDS_INT32, n_frames, 0, &enc);
-    if (rc == RT_OK) ctx->pixels += (uint64_t)nb * band_rows * width * (uint64_t)n_frames;
+    if (rc == RT_OK) {
+        ctx->pixels += (uint64_t)nb * band_rows * width * (uint64_t)n_frames;
+        if (frame0 == 0 || !d.staged.valid || d.staged.wire != d_wire)
+            d.staged = {true, width, height, band_rows, rank, world, batch_frames, d_wire};
+    }
     return rc;
 }
 
@@ -994,10 +1006,17 @@ int rt_finish_wire(rt_ctx* ctx, int width, int height, int band_rows, int rank, 
     if (!codec_geom(width, height, band_rows, world, n_frames, g, nullptr) || rank < 0 || rank >= world ||
         !d_wire || ((uintptr_t)d_wire & 7) != 0)
         return fail(ctx, RT_ERR_INVALID_ARG, "rt_finish_wire: bad arguments");
+    if (ctx->n_gpus != 1) return fail(ctx, RT_ERR_INVALID_ARG, "rt_finish_wire needs a single-GPU context");
     Device& d = ctx->dev[0];
     DeviceGuard guard(d.id);
-    if (!d.d_stage || encode_stage_bytes(g) > d.stage_cap)
-        return fail(ctx, RT_ERR_INVALID_ARG, "rt_finish_wire: no rt_render_bands_tiles batch of %d frames", n_frames);
+    // only the batch rt_render_bands_tiles staged last, with the same geometry and wire
+    const auto& sb = d.staged;
+    if (!d.d_stage || encode_stage_bytes(g) > d.stage_cap || !sb.valid || sb.W != width || sb.H != height ||
+        sb.band_rows != band_rows || sb.rank != rank || sb.world != world || sb.wire != d_wire ||
+        n_frames > sb.batch_frames)
+        return fail(ctx, RT_ERR_INVALID_ARG,
+                    "rt_finish_wire: no rt_render_bands_tiles batch of this geometry and wire with >= %d frames",
+                    n_frames);
     const int traced_rows = (bands_of(height, band_rows, rank, world) * band_rows + 7) / 8;
     int e = launch_finish_wire((unsigned char*)d_wire, g, traced_rows, d_wire_bytes, d.d_stage, hip_stream);
     if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "finish launch: %s", hipGetErrorString((hipError_t)e));

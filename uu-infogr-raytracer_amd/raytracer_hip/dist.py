@@ -331,6 +331,13 @@ class TileBandGather:
         self.capacity_per_frame = None  # speculative gather size (set_capacity); None = wait for the size
         self.redone = 0        # batches whose wire outgrew the speculative size (gathered again)
         self.decode_batch = -1  # the batch of the decode being issued
+        # Speculative batches are decoded before their reduced size is known: until _stage_c has checked
+        # it, the batch's ring and decoded_ev[b] are provisional (a wire cut short decoded stale payload
+        # bytes).  Invariant: once _stage_c(b) returns, decoded_ev[b] is the event of the decode that
+        # stands (a redo's second decode replaces the first one's event, which only the redo gather --
+        # reader=b, the receive buffer's last reader -- waits on); ring_of refuses provisional batches.
+        self.provisional = set()
+        self.decodes_of = {}    # batch -> decodes issued (2 for a redone speculative batch)
 
     def set_capacity(self, margin=1.25):
         """From now on gather each batch with a speculative size -- `margin` x the largest wire per
@@ -384,6 +391,8 @@ class TileBandGather:
         return dist.gather(self.wire[i][:n], glist, dst=0, async_op=True)
 
     def ring_of(self, batch):
+        if batch in self.provisional:
+            raise RuntimeError(f"batch {batch}: decoded speculatively, its size not yet checked")
         return self.frames[batch % 3]
 
     def wire_target(self, k=None):
@@ -490,6 +499,7 @@ class TileBandGather:
         else:  # speculative gather: the reduced size decides whether it sufficed
             work, n_spec, decode_first = spec
             if decode_first:  # (a wire cut short decodes stale payload bytes inside its own slot)
+                self.provisional.add(b)
                 self._decode(b, n_frames, gw)
             n = self._read_size(b % 3, work)
             self.max_per_frame = max(self.max_per_frame, n / n_frames)
@@ -500,6 +510,7 @@ class TileBandGather:
                 self.bytes_sent += n
             if n > n_spec or not decode_first:
                 self._decode(b, n_frames, gw)
+            self.provisional.discard(b)  # the decode that stands has been issued
         if self.root:
             self.decoded += 1
 
@@ -509,6 +520,7 @@ class TileBandGather:
         that stands (`decode_batch` names the batch being decoded)."""
         import torch
         self.decode_batch = b
+        self.decodes_of[b] = self.decodes_of.get(b, 0) + 1
         if self.cuda:
             with torch.cuda.stream(self.dec):
                 gw.wait()
@@ -516,7 +528,7 @@ class TileBandGather:
                 ev.record(self.dec)
                 self.gathered_ev[b] = ev
                 if self.root:
-                    self.decode(self.recv[b % 2], self.rank_stride, n_frames, self.ring_of(b), self.dec,
+                    self.decode(self.recv[b % 2], self.rank_stride, n_frames, self.frames[b % 3], self.dec,
                                 self.first_rank)
                     dv = torch.cuda.Event()
                     dv.record(self.dec)
@@ -525,7 +537,7 @@ class TileBandGather:
             gw.wait()
             self.gathered_ev[b] = None
             if self.root:
-                self.decode(self.recv[b % 2], self.rank_stride, n_frames, self.ring_of(b), None, self.first_rank)
+                self.decode(self.recv[b % 2], self.rank_stride, n_frames, self.frames[b % 3], None, self.first_rank)
                 self.decoded_ev[b] = None
 
     def commit(self, main=None):
