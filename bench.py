@@ -95,6 +95,10 @@ def parse(argv=None):
                     help="N>1 tiles: rank 0 traces nothing and assembles the frames that ranks 1..N-1 "
                          "trace as a band world of N-1 (auto: N >= 8, where rank 0's own share plus the "
                          "decode of the others' made it the slowest rank)")
+    ap.add_argument("--torch-collectives", action="store_true",
+                    help="N>1 tiles: the size reduce and the gather through torch.distributed (its own collective "
+                         "stream, waited on side streams) also for a run of one batch, instead of the library's RCCL "
+                         "communicator on the trace/encode/decode stream (rt_comm_*)")
     ap.add_argument("--dist-path", action="store_true",
                     help="rehearsal: run the N>1 band/gather path even with one process (RCCL world of 1)")
     ap.add_argument("--verify", action="store_true",
@@ -502,10 +506,19 @@ def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, s
                 ctx.decode_gathered(W, H, rb.band_rows, band_world, recv.data_ptr(), rank_stride, n, frames_.data_ptr(),
                                     W * H, st.cuda_stream, first_rank=first_rank)
 
+            coll = None
+            if not args.rehearse_gloo and not args.torch_collectives and args.batch >= args.steps:
+                # a run of one batch (the driver's --steps 20; each warm-up batch is drained too): the size
+                # reduce and the gather through the library's RCCL communicator on the stream that traces,
+                # encodes and decodes -- no hops into and out of torch.distributed's collective stream
+                # (~20 us each, profiles/r03_dist_stages.txt).  Pipelined runs keep torch.distributed on
+                # side streams, where the gather of batch b-1 overlaps the trace of batch b.
+                from raytracer_hip.dist import LibraryCollectives
+                coll = LibraryCollectives(ctx, rank, world, lambda t: dist.broadcast(t, src=0))
             tg = TileBandGather(rb, torch.device("cuda", local), args.batch,
                                 lambda n: wire_layout(W, H, rb.band_rows, band_world, n), t_encode, t_decode,
                                 rank0_codec=args.rank0_codec, compositor=comp, phys_rank=rank, phys_world=world,
-                                fused=not args.no_fuse)
+                                fused=not args.no_fuse, coll=coll, main_stream=stream)
             out_fmt = abi.RT_BANDS_FRAME if tg.direct else abi.RT_BANDS_INT32
             # frames alternate between trace streams (two in flight per rank); at a batch end the
             # encode runs on `stream` after the others joined it, and the trace streams then wait
@@ -721,6 +734,8 @@ def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, s
                 "lights": len(sc.lights), "depth": sc.recursion_limit + 1,
                 "parallelism": f"interleaved {args.band_rows}-row bands x {world - 1 if comp else world} ranks + RCCL gather to "
                 f"rank 0{' (compositor: rank 0 decodes, ranks 1..N-1 trace)' if comp else ''}"
+                + (" [collectives: " + ("library RCCL on the trace stream" if (tg is not None and tg.coll is not None)
+                                        else "torch.distributed") + "]")
                 + (" (one gather per frame)" if args.no_pipeline else
                    f" ({args.batch} frames per gather, {args.band_format} bands, double-buffered: the gather of "
                    f"one batch overlaps the trace of the next)"),

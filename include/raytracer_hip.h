@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 6
+#define RT_ABI_VERSION 7
 
 /* ---- status codes ---------------------------------------------------------- */
 enum {
@@ -279,6 +279,27 @@ int rt_render_bands_tiles(rt_ctx* ctx, int width, int height, int band_rows, int
                           int frame0, int n_frames, int batch_frames, void* d_wire, void* hip_stream);
 int rt_finish_wire(rt_ctx* ctx, int width, int height, int band_rows, int rank, int world, int n_frames,
                    void* d_wire, int64_t* d_wire_bytes, void* hip_stream);
+
+/* ---- one-process-per-GPU collectives on the trace stream (ABI 7) ---------------- */
+/* The N > 1 tile pipeline's two exchange steps -- the all_reduce(MAX) of the wire sizes and the
+ * gather of every rank's wire to rank 0 (the reference's only parallel loop is
+ * RayTracer.cs:898-901) -- issued by the library itself on the caller's HIP stream, the stream
+ * that traced and encoded the batch and that decodes it, so the exchange adds no cross-stream
+ * hops (a torch.distributed collective runs on its own stream: a wait into it and one out of it,
+ * ~20 us each in profiles/r03_dist_stages.txt).  The communicator is RCCL (the instance already
+ * loaded in the process when there is one), one rank per process and device:
+ *   rank 0: rt_comm_unique_id(id); share the RT_COMM_ID_BYTES with every rank (e.g. a broadcast);
+ *   every rank: rt_comm_init(ctx, world, rank, id)          -- collective, on ctx's device. */
+#define RT_COMM_ID_BYTES 128
+int rt_comm_unique_id(void* out_id);
+int rt_comm_init(rt_ctx* ctx, int world, int rank, const void* id);
+/* In place, count int64 values on the device: every rank ends with the element-wise maximum. */
+int rt_comm_allreduce_max_i64(rt_ctx* ctx, int64_t* d_values, int count, void* hip_stream);
+/* Gather n_bytes from every rank's d_send to rank 0: rank r's bytes land at
+ * d_recv + ((r - rotate) mod world) * recv_stride (rank 0 only; its own by a device copy).
+ * Collective; n_bytes must be the same on every rank (0: nothing moves). */
+int rt_comm_gather(rt_ctx* ctx, const void* d_send, size_t n_bytes, void* d_recv, size_t recv_stride, int rotate,
+                   void* hip_stream);
 
 /* ---- double-buffered frames ------------------------------ */
 /* Asynchronous Tick(): captures the current camera, enqueues the trace and the D2H copy

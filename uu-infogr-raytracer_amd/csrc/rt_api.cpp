@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <dlfcn.h>
+#include <link.h>
 #include <new>
 #include <string>
 #include <vector>
@@ -31,7 +32,20 @@ using namespace rtk;
 namespace {
 typedef void* ncclComm_t;
 typedef int ncclResult_t;
-enum { ncclInt32 = 2 };
+enum { ncclUint8 = 1, ncclInt32 = 2, ncclInt64 = 4 };
+enum { ncclMax = 2 };
+struct ncclUniqueId {
+    char internal[RT_COMM_ID_BYTES];
+};
+// The librccl already mapped into the process (torch's, in a torch.distributed job), so that our
+// communicator and the framework's share one RCCL instance; else the first that dlopen finds.
+int find_loaded_rccl(struct dl_phdr_info* info, size_t, void* out) {
+    if (info->dlpi_name && std::strstr(info->dlpi_name, "librccl")) {
+        *(std::string*)out = info->dlpi_name;
+        return 1;
+    }
+    return 0;
+}
 struct Rccl {
     void* h = nullptr;
     ncclResult_t (*CommInitAll)(ncclComm_t*, int, const int*) = nullptr;
@@ -39,12 +53,20 @@ struct Rccl {
     ncclResult_t (*Gather)(const void*, void*, size_t, int, int, ncclComm_t, hipStream_t) = nullptr;
     ncclResult_t (*GroupStart)() = nullptr;
     ncclResult_t (*GroupEnd)() = nullptr;
+    ncclResult_t (*GetUniqueId)(ncclUniqueId*) = nullptr;
+    ncclResult_t (*CommInitRank)(ncclComm_t*, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*AllReduce)(const void*, void*, size_t, int, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Send)(const void*, size_t, int, int, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*Recv)(void*, size_t, int, int, ncclComm_t, hipStream_t) = nullptr;
     const char* (*GetErrorString)(ncclResult_t) = nullptr;
     bool load(std::string& err) {
         if (h) return true;
+        std::string loaded;
+        dl_iterate_phdr(find_loaded_rccl, &loaded);
+        if (!loaded.empty()) h = dlopen(loaded.c_str(), RTLD_NOW | RTLD_NOLOAD);
         const char* names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
         for (const char* n : names)
-            if ((h = dlopen(n, RTLD_NOW | RTLD_GLOBAL))) break;
+            if (!h && (h = dlopen(n, RTLD_NOW | RTLD_GLOBAL))) break;
         if (!h) {
             err = "dlopen(librccl) failed";
             return false;
@@ -54,9 +76,15 @@ struct Rccl {
         Gather = (decltype(Gather))dlsym(h, "ncclGather");
         GroupStart = (decltype(GroupStart))dlsym(h, "ncclGroupStart");
         GroupEnd = (decltype(GroupEnd))dlsym(h, "ncclGroupEnd");
+        GetUniqueId = (decltype(GetUniqueId))dlsym(h, "ncclGetUniqueId");
+        CommInitRank = (decltype(CommInitRank))dlsym(h, "ncclCommInitRank");
+        AllReduce = (decltype(AllReduce))dlsym(h, "ncclAllReduce");
+        Send = (decltype(Send))dlsym(h, "ncclSend");
+        Recv = (decltype(Recv))dlsym(h, "ncclRecv");
         GetErrorString = (decltype(GetErrorString))dlsym(h, "ncclGetErrorString");
-        if (!CommInitAll || !CommDestroy || !Gather || !GroupStart || !GroupEnd) {
-            err = "librccl lacks ncclCommInitAll/ncclGather/ncclGroupStart";
+        if (!CommInitAll || !CommDestroy || !Gather || !GroupStart || !GroupEnd || !GetUniqueId || !CommInitRank ||
+            !AllReduce || !Send || !Recv) {
+            err = "librccl lacks a symbol (ncclCommInitAll/InitRank/GetUniqueId/Gather/AllReduce/Send/Recv/Group*)";
             return false;
         }
         return true;
@@ -112,6 +140,7 @@ struct Device {
     std::vector<EventPair> pending, pool;
     uint64_t op_count[3] = {0, 0, 0};  // operations per timing kind (sampling phase)
     ncclComm_t comm = nullptr;
+    int comm_rank = 0, comm_world = 0;  // rt_comm_init (one rank per process); 0 = none
 };
 
 struct SceneLayout {
@@ -1040,6 +1069,80 @@ int rt_decode_gathered(rt_ctx* ctx, int width, int height, int band_rows, int wo
     DeviceGuard guard(d.id);
     int e = launch_decode_gathered((const unsigned char*)d_gathered, rank_stride, d_frames, g, hip_stream);
     if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "decode launch: %s", hipGetErrorString((hipError_t)e));
+    return RT_OK;
+}
+
+int rt_comm_unique_id(void* out_id) {
+    if (!out_id) return fail(nullptr, RT_ERR_INVALID_ARG, "rt_comm_unique_id: NULL");
+    std::string err;
+    if (!g_rccl.load(err)) return fail(nullptr, RT_ERR_RCCL, "%s", err.c_str());
+    ncclUniqueId id;
+    const ncclResult_t r = g_rccl.GetUniqueId(&id);
+    if (r != 0) return fail(nullptr, RT_ERR_RCCL, "ncclGetUniqueId: %s", g_rccl.GetErrorString ? g_rccl.GetErrorString(r) : "?");
+    std::memcpy(out_id, id.internal, RT_COMM_ID_BYTES);
+    return RT_OK;
+}
+
+int rt_comm_init(rt_ctx* ctx, int world, int rank, const void* id) {
+    if (!ctx || !id || world < 1 || rank < 0 || rank >= world)
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_comm_init: bad arguments");
+    if (ctx->n_gpus != 1 || ctx->rccl_gather)
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_comm_init needs a single-GPU context without RT_CREATE_RCCL_GATHER");
+    Device& d = ctx->dev[0];
+    if (d.comm) return fail(ctx, RT_ERR_INVALID_ARG, "rt_comm_init: the context already has a communicator");
+    std::string err;
+    if (!g_rccl.load(err)) return fail(ctx, RT_ERR_RCCL, "%s", err.c_str());
+    DeviceGuard guard(d.id);
+    ncclUniqueId uid;
+    std::memcpy(uid.internal, id, RT_COMM_ID_BYTES);
+    const ncclResult_t r = g_rccl.CommInitRank(&d.comm, world, uid, rank);
+    if (r != 0) {
+        d.comm = nullptr;
+        return fail(ctx, RT_ERR_RCCL, "ncclCommInitRank: %s", g_rccl.GetErrorString ? g_rccl.GetErrorString(r) : "?");
+    }
+    d.comm_rank = rank, d.comm_world = world;
+    return RT_OK;
+}
+
+int rt_comm_allreduce_max_i64(rt_ctx* ctx, int64_t* d_values, int count, void* hip_stream) {
+    if (!ctx || !d_values || count < 1) return fail(ctx, RT_ERR_INVALID_ARG, "rt_comm_allreduce_max_i64: bad arguments");
+    Device& d = ctx->dev[0];
+    if (!d.comm || !d.comm_world) return fail(ctx, RT_ERR_INVALID_ARG, "rt_comm_allreduce_max_i64: no rt_comm_init");
+    DeviceGuard guard(d.id);
+    const ncclResult_t r =
+        g_rccl.AllReduce(d_values, d_values, (size_t)count, ncclInt64, ncclMax, d.comm, (hipStream_t)hip_stream);
+    if (r != 0) return fail(ctx, RT_ERR_RCCL, "ncclAllReduce: %s", g_rccl.GetErrorString ? g_rccl.GetErrorString(r) : "?");
+    return RT_OK;
+}
+
+int rt_comm_gather(rt_ctx* ctx, const void* d_send, size_t n_bytes, void* d_recv, size_t recv_stride, int rotate,
+                   void* hip_stream) {
+    if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "NULL context");
+    Device& d = ctx->dev[0];
+    if (!d.comm || !d.comm_world) return fail(ctx, RT_ERR_INVALID_ARG, "rt_comm_gather: no rt_comm_init");
+    const int world = d.comm_world, rank = d.comm_rank;
+    if ((n_bytes && !d_send) || (rank == 0 && n_bytes && (!d_recv || recv_stride < n_bytes)))
+        return fail(ctx, RT_ERR_INVALID_ARG, "rt_comm_gather: bad arguments");
+    if (!n_bytes) return RT_OK;
+    DeviceGuard guard(d.id);
+    const hipStream_t st = (hipStream_t)hip_stream;
+    auto slot = [&](int r) { return (size_t)(((r - rotate) % world + world) % world) * recv_stride; };
+    if (world > 1) {
+        if (g_rccl.GroupStart() != 0) return fail(ctx, RT_ERR_RCCL, "ncclGroupStart failed");
+        ncclResult_t r = 0;
+        if (rank != 0) {
+            r = g_rccl.Send(d_send, n_bytes, ncclUint8, 0, d.comm, st);
+        } else {
+            for (int q = 1; q < world && r == 0; ++q)
+                r = g_rccl.Recv((char*)d_recv + slot(q), n_bytes, ncclUint8, q, d.comm, st);
+        }
+        const ncclResult_t e = g_rccl.GroupEnd();
+        if (r != 0 || e != 0)
+            return fail(ctx, RT_ERR_RCCL, "ncclSend/Recv: %s",
+                        g_rccl.GetErrorString ? g_rccl.GetErrorString(r ? r : e) : "?");
+    }
+    if (rank == 0)  // rank 0's own slot
+        HIP_TRY(ctx, hipMemcpyAsync((char*)d_recv + slot(0), d_send, n_bytes, hipMemcpyDeviceToDevice, st));
     return RT_OK;
 }
 

@@ -198,6 +198,26 @@ class Context:
         self._check(self.lib.rt_finish_wire(self.ptr, width, height, band_rows, rank, world, n_frames,
                                             C.c_void_p(d_wire), C.c_void_p(d_wire_bytes or None), C.c_void_p(stream)))
 
+    # -- one-process-per-GPU collectives on the caller's stream (rt_comm_*) --------------
+    def comm_unique_id(self) -> bytes:
+        """A new RCCL unique id (rank 0), to be shared with every rank (rt_comm_unique_id)."""
+        buf = C.create_string_buffer(abi.RT_COMM_ID_BYTES)
+        self._check(self.lib.rt_comm_unique_id(buf))
+        return buf.raw
+
+    def comm_init(self, world: int, rank: int, uid: bytes):
+        """Join this context's device to a communicator of `world` ranks (collective; rt_comm_init)."""
+        assert len(uid) == abi.RT_COMM_ID_BYTES
+        self._check(self.lib.rt_comm_init(self.ptr, world, rank, C.create_string_buffer(uid, abi.RT_COMM_ID_BYTES)))
+
+    def comm_allreduce_max_i64(self, d_ptr: int, count: int, stream: int = 0):
+        self._check(self.lib.rt_comm_allreduce_max_i64(self.ptr, C.c_void_p(d_ptr), count, C.c_void_p(stream)))
+
+    def comm_gather(self, d_send: int, n_bytes: int, d_recv: int, recv_stride: int, rotate: int = 0, stream: int = 0):
+        """n_bytes of every rank's d_send to rank 0's d_recv slots ((r - rotate) mod world) * recv_stride."""
+        self._check(self.lib.rt_comm_gather(self.ptr, C.c_void_p(d_send), n_bytes, C.c_void_p(d_recv or None),
+                                            recv_stride, rotate, C.c_void_p(stream)))
+
     def render_async(self, width: int, height: int, out: np.ndarray):
         """Double-buffered Tick (rt_render_async): returns at once; `wait()` before reading `out`."""
         assert out.dtype == np.int32 and out.flags.c_contiguous and out.size == width * height

@@ -282,7 +282,7 @@ class TileBandGather:
     """
 
     def __init__(self, rb: RowBands, device, frames_per_batch, layout_fn, encode, decode, rank0_codec=False,
-                 compositor=False, phys_rank=None, phys_world=None, fused=False):
+                 compositor=False, phys_rank=None, phys_world=None, fused=False, coll=None, main_stream=None):
         import torch
         self.rb, self.F, self.device = rb, max(1, frames_per_batch), torch.device(device)
         self.cuda = self.device.type == "cuda"
@@ -315,8 +315,15 @@ class TileBandGather:
         self.frame_elems = rb.width * rb.height
         self.frames = ([torch.zeros(self.F * self.frame_elems, dtype=torch.int32, device=self.device)
                         for _ in range(3)] if self.root else None)
+        # coll (GPUs): the library's collectives (LibraryCollectives) issued on `main_stream`, the
+        # stream that encodes and now also gathers and decodes -- no hops into and out of the
+        # framework's collective stream; else torch.distributed, waited on two side streams
+        self.coll = coll if self.cuda else None
         if self.cuda:
-            self.comm, self.dec = torch.cuda.Stream(self.device), torch.cuda.Stream(self.device)
+            if self.coll is not None:
+                self.comm = self.dec = main_stream if main_stream is not None else torch.cuda.current_stream(self.device)
+            else:
+                self.comm, self.dec = torch.cuda.Stream(self.device), torch.cuda.Stream(self.device)
             self.enc_events = [torch.cuda.Event() for _ in range(4)]
         self.k = 0             # frames rendered
         self.batch = 0         # batches encoded
@@ -387,6 +394,9 @@ class TileBandGather:
                     self.comm.wait_event(self.decoded_ev[reader])
                 for old in [x for x in self.decoded_ev if x < b - 4]:
                     del self.decoded_ev[old]
+                if self.coll is not None:
+                    return self.coll.gather(self.wire[i], n, self.recv[j] if self.root else None, self.rank_stride,
+                                            1 if self.compositor else 0, self.comm)
                 return dist.gather(self.wire[i][:n], glist, dst=0, async_op=True)
         return dist.gather(self.wire[i][:n], glist, dst=0, async_op=True)
 
@@ -472,12 +482,18 @@ class TileBandGather:
             # checks the reduced size (and gathers + decodes again if it was exceeded)
             n = self._spec_bytes(n_frames)
             gw = self._gather(b, i, n)
-            work = dist.all_reduce(self.size[i], op=dist.ReduceOp.MAX, async_op=True)
+            work = self._size_reduce(i)
             self.stage_c.append((b, n_frames, gw, (work, n, True)))
         else:
-            work = dist.all_reduce(self.size[i], op=dist.ReduceOp.MAX, async_op=True)
+            work = self._size_reduce(i)
             self.stage_b.append((b, n_frames, work))
         self.batch += 1
+    def _size_reduce(self, i):
+        import torch.distributed as dist
+        if self.coll is not None:
+            return self.coll.all_reduce_max(self.size[i], self.comm)
+        return dist.all_reduce(self.size[i], op=dist.ReduceOp.MAX, async_op=True)
+
     def _stage_b(self):
         b = self.stage_b[0][0]
         while self.stage_c and self.stage_c[0][0] <= b - 2:  # receive buffer b % 2 is free again
@@ -558,3 +574,36 @@ class TileBandGather:
             self._stage_b()
         while self.stage_c:
             self._stage_c()
+
+
+class _Done:
+    """A collective issued on the stream that consumes it: nothing to wait for."""
+
+    def wait(self):
+        return None
+
+
+class LibraryCollectives:
+    """TileBandGather's two exchange steps through the HIP library's own communicator (rt_comm_*:
+    RCCL on the caller's stream) instead of torch.distributed's collective stream.
+
+    Every rank builds one (collective: rank 0 makes the unique id and broadcasts it over the
+    process group `pg_broadcast(tensor)`)."""
+
+    def __init__(self, ctx, rank, world, broadcast):
+        import torch
+        uid = torch.zeros(128, dtype=torch.uint8, device="cuda")
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(ctx.comm_unique_id()), dtype=torch.uint8))
+        broadcast(uid)
+        ctx.comm_init(world, rank, bytes(uid.cpu().numpy().tobytes()))
+        self.ctx = ctx
+
+    def all_reduce_max(self, t, stream):
+        self.ctx.comm_allreduce_max_i64(t.data_ptr(), t.numel(), stream.cuda_stream)
+        return _Done()
+
+    def gather(self, send, n, recv, stride, rotate, stream):
+        self.ctx.comm_gather(send.data_ptr(), n, recv.data_ptr() if recv is not None else 0, stride, rotate,
+                             stream.cuda_stream)
+        return _Done()
