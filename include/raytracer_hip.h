@@ -302,15 +302,19 @@ int rt_comm_gather(rt_ctx* ctx, const void* d_send, size_t n_bytes, void* d_recv
                    void* hip_stream);
 
 /* ---- double-buffered frames ------------------------------ */
-/* Asynchronous Tick(): captures the current camera, enqueues the trace and the D2H copy
- * into the caller's host buffer pixels[width*height] and returns at once.  rt_wait blocks
- * until every enqueued frame is complete.  With two host buffers a caller overlaps the
- * trace of frame k+1 with its own use of frame k (the camera of k+1 can already be set).
- * The context keeps two device frame buffers, a trace stream and a copy stream: frame k+1's
- * trace overlaps frame k's D2H copy (1080p C2: 190 us per frame with two frames in flight
- * and an rt_wait per pair, against 200 us for rt_render).  Frames complete in order;
- * rt_wait returns when every enqueued frame is complete.
- * Multi-GPU contexts render synchronously here (rt_render). */
+/* Asynchronous Tick(): captures the current camera, enqueues the trace and returns at once;
+ * rt_wait blocks until every enqueued frame is in its host buffer.  With two host buffers a
+ * caller overlaps the trace of frame k+1 with its own use of frame k (the camera of k+1 can
+ * already be set).  One in-order stream and two device frame buffers: frame k's D2H copy rides
+ * in frame k+1's launch (a copy slice dispatched ahead of the trace workgroups, so the PCIe-bound
+ * copy runs under the next trace) or is issued by rt_wait, rt_render, rt_unregister_host or
+ * rt_destroy.  The slice writes only host buffers registered with rt_register_host (through their
+ * device-mapped address); any other buffer gets hipMemcpyAsync on the same stream.  Measured on
+ * MI355X at 1080p C2 (bench.py tick_*, median of 3 x 20 frames): a display loop two frames deep
+ * (rt_wait per pair) 5.2-5.3k fps, 20 frames queued 5.4-5.5k fps, against 4.9-5.0k for the
+ * synchronous rt_render; a trace stream plus a copy stream ordered by events (round 2) ran
+ * 1.5-5.2k fps depending on the process (profiles/r03_tick_ab.txt).  Multi-GPU contexts render
+ * synchronously here (rt_render). */
 int rt_render_async(rt_ctx* ctx, int width, int height, int32_t* pixels);
 int rt_wait(rt_ctx* ctx);
 

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round 3: the fused Tick hand-off -- its GPU tests first, then the whole GPU suite, the hand-off probe
 # (fused vs RT_ASYNC_NOFUSE, i.e. one stream with the runtime's copy) and the default bench line.
+# (historical: RT_ASYNC_NOFUSE was removed after this A/B; profiles/r03_tick_ab.txt holds its output)
 set -eo pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
 O=$R/gpurun_out/r03a

@@ -1,5 +1,6 @@
 #!/bin/bash
 # A/B of rt_render_async's hand-off (RT_ASYNC_MODE: 0 two streams + events, 1 one stream, 2 zero-copy), no profiler.
+# (historical: RT_ASYNC_MODE was removed from rt_api.cpp after this A/B; profiles/r03_tick_ab.txt holds its output)
 set -eo pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}
 mkdir -p $R/gpurun_out/tick_ab

@@ -1257,10 +1257,10 @@ int rt_render(rt_ctx* ctx, int width, int height, int32_t* pixels) {
 // issued by rt_wait.  Buffer k % 2 is traced again by launch k+2, after launch k+1 (its copy) on the
 // same stream.  The slice writes only host ranges registered through rt_register_host (their
 // device-mapped addresses); any other buffer gets hipMemcpyAsync on the same stream.
-// Measured before (tools/tick_ab.sh, profiles/r03_tick_ab.txt): a trace stream and a copy stream
-// ordered by events ran 175-195 us per frame in some processes and 350-1200 us in others -- torch's
-// own kernel-on-one-stream / D2H-on-another pattern does the same -- while one stream ran a steady
-// 195-200 us (trace, then the runtime's copy kernel, no overlap).
+// Measured (profiles/r03_tick_ab.txt): a trace stream and a copy stream ordered by events ran
+// 175-195 us per frame in some processes and 350-1200 us in others -- torch's own kernel-on-one-
+// stream / D2H-on-another pattern does the same -- while one stream ran a steady 195-200 us with
+// the runtime's copy and 184-187 us with the copy slice.
 int rt_render_async(rt_ctx* ctx, int width, int height, int32_t* pixels) {
     int rc = check_ctx(ctx, width, height);
     if (rc != RT_OK) return rc;
@@ -1278,15 +1278,10 @@ int rt_render_async(rt_ctx* ctx, int width, int height, int32_t* pixels) {
     }
     rc = grow(ctx, (void**)&d.d_frames2[slot], &d.frames2_cap[slot], frame_bytes);
     if (rc != RT_OK) return rc;
-    static const bool nofuse = getenv("RT_ASYNC_NOFUSE") != nullptr;  // A/B probe only
-    if (nofuse) {
-        rc = flush_hand(ctx);
-        if (rc != RT_OK) return rc;
-    }
     rc = trace_bands(ctx, d, d.async_stream, width, height, height, 0, 1, d.d_frames2[slot], nullptr, RT_BANDS_INT32,
                      1, 0, nullptr, true);
     if (rc != RT_OK) return rc;
-    int32_t* mapped = nofuse ? nullptr : mapped_host(ctx, pixels, frame_bytes);
+    int32_t* mapped = mapped_host(ctx, pixels, frame_bytes);
     if (mapped) {
         d.hand.host = pixels;
         d.hand.mapped = mapped;
