@@ -2,6 +2,7 @@
 drivers against each other, the independent numpy float32 emulation, and the committed
 golden fixtures.  (No GPU; the reference ships no tests of its own -- parity unpinned.)"""
 import math
+import os
 import zlib
 
 import numpy as np
@@ -171,3 +172,27 @@ def test_oracle_segments_count_every_visible_ray(oracle, cid, w, h):
     prim = seg[seg["kind"] == 0]
     assert np.array_equal(prim["pixel"], np.arange(w * h))
     assert np.all(np.diff(seg["pixel"]) >= 0)  # walk order, pixel by pixel
+
+
+def test_full_size_goldens_pinned_by_the_all_hit_driver():
+    """tests/golden/pin_allhit.log (make_golden.py --pin): every full-size golden CRC -- C4 3840x2160 and
+    C5 7680x4320 included -- was re-derived by the reference-faithful all-hit driver (every hit shaded,
+    RayTracer.cs:975-991, 792-823) and equals the nearest driver's and golden.json's, and the numpy
+    emulation agrees on the C4/C5 scene at 384x216.  The log must cover every golden full-size case."""
+    import json
+    import re
+    here = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+    gold = json.load(open(os.path.join(here, "golden.json")))["cases"]
+    log = open(os.path.join(here, "pin_allhit.log")).read().splitlines()
+    seen = {}
+    for line in log:
+        m = re.match(r"(\S+)\s+(\d+)x(\d+) all-hit ([0-9a-f]{8}) nearest ([0-9a-f]{8}) golden ([0-9a-f]{8}) "
+                     r"mismatching pixels (\d+) (OK|FAIL)", line)
+        if m:
+            seen[m.group(1)] = m
+    for cid in ("REF_512", "REF_1280x720", "C1", "C2", "C3", "C4", "C5"):
+        m = seen[cid]
+        assert m.group(8) == "OK" and m.group(7) == "0"
+        assert m.group(4) == m.group(5) == m.group(6) == gold[cid]["crc32"], cid
+        assert (int(m.group(2)), int(m.group(3))) == (gold[cid]["width"], gold[cid]["height"])
+    assert any(line.startswith("C4/C5 scene") and line.rstrip().split()[-3] == "OK" for line in log)
