@@ -400,11 +400,12 @@ def main():
             print(f"bench.py --gpus {args.gpus}: only {n} GPU(s) visible", file=sys.stderr, flush=True)
             sys.exit(2)
         sys.exit(subprocess.call(launch_command(sys.argv[1:], args.gpus, args.master_port)))
+    args.auto_batch = args.batch <= 0
     if args.batch <= 0:
         # N > 1: a short run is one batch (one size reduce + one gather + one decode: the fixed
         # latency of each collective and of the host's size read-back dominates a handful of
         # 1080p frames, and a pipeline of small batches pays it per batch); long runs pipeline
-        # batches of 64 frames
+        # batches of 64 frames.  The tile pipeline refines this per leg (auto_batch_frames).
         args.batch = args.steps if args.steps <= 128 else 64
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -438,10 +439,40 @@ def main():
         o2 = dist_leg(args, name, rank, world, local, torch, dist, Context, abi, scenes)
         if rank == 0:
             out.setdefault("also", {})[o2["config"]["workload"].split(":")[0]] = {
-                k: o2[k] for k in ("value", "unit", "n_gpus", "steps", "ms_per_step", "fps", "config", "roofline")}
+                k: o2[k] for k in ("value", "unit", "n_gpus", "steps", "ms_per_step", "fps", "config", "roofline",
+                                   "verified_frames") if k in o2}
     if rank == 0:
         print(json.dumps(out), flush=True)
     dist.destroy_process_group()
+
+
+def auto_batch_frames(ctx, W, H, rb, band_rank, band_world, idle, steps, torch, dist, target_s=1e-3, max_batches=4):
+    """Frames per gather for a run of `steps` <= 128 frames (every rank takes part; all get the same
+    answer).  One batch when the run's trace is short (C2: the fixed latency of each collective, the
+    size read-back and the decode dominate, and one batch can use the library's collectives on the
+    trace stream); otherwise up to `max_batches` batches of >= `target_s` of trace each, so that the
+    gather and rank 0's decode of batch b run under the trace of batch b+1 instead of after the whole
+    run (C5: a 1080p-sized wire per rank per frame is megabytes -- ~1 ms of gather and 0.7 ms of
+    decode for 20 frames at N = 8, ~3.7 ms of gather over one link at N = 2).  The per-frame trace time
+    of this rank's share comes from a 2-frame launch after a warm one, the max over ranks."""
+    import time as _t
+    t = 0.0
+    if not idle and rb.slot_elems > 0:
+        from raytracer_hip import abi as _abi
+        buf = torch.empty(2 * rb.slot_elems, dtype=torch.int32, device="cuda")
+        st = torch.cuda.current_stream().cuda_stream
+        for rep in range(2):
+            torch.cuda.synchronize()
+            t0 = _t.perf_counter()
+            ctx.render_bands_batch(W, H, rb.band_rows, band_rank, band_world, 2, buf.data_ptr(), rb.slot_elems * 4,
+                                   _abi.RT_BANDS_INT32, st)
+            torch.cuda.synchronize()
+            t = (_t.perf_counter() - t0) / 2
+        del buf
+    tt = torch.tensor([t], dtype=torch.float64, device="cuda")
+    dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+    k = max(1, min(max_batches, int(round(steps * float(tt) / target_s))))
+    return -(-steps // k)
 
 
 def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, scenes, size=""):
@@ -506,8 +537,12 @@ def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, s
                 ctx.decode_gathered(W, H, rb.band_rows, band_world, recv.data_ptr(), rank_stride, n, frames_.data_ptr(),
                                     W * H, st.cuda_stream, first_rank=first_rank)
 
+            batch = args.batch
+            if args.auto_batch and args.steps <= 128:
+                batch = auto_batch_frames(ctx, W, H, rb, band_rank, band_world, comp and rank == 0, args.steps,
+                                          torch, dist)
             coll = None
-            if not args.rehearse_gloo and not args.torch_collectives and args.batch >= args.steps:
+            if not args.rehearse_gloo and not args.torch_collectives and batch >= args.steps:
                 # a run of one batch (the driver's --steps 20; each warm-up batch is drained too): the size
                 # reduce and the gather through the library's RCCL communicator on the stream that traces,
                 # encodes and decodes -- no hops into and out of torch.distributed's collective stream
@@ -515,7 +550,7 @@ def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, s
                 # side streams, where the gather of batch b-1 overlaps the trace of batch b.
                 from raytracer_hip.dist import LibraryCollectives
                 coll = LibraryCollectives(ctx, rank, world, lambda t: dist.broadcast(t, src=0))
-            tg = TileBandGather(rb, torch.device("cuda", local), args.batch,
+            tg = TileBandGather(rb, torch.device("cuda", local), batch,
                                 lambda n: wire_layout(W, H, rb.band_rows, band_world, n), t_encode, t_decode,
                                 rank0_codec=args.rank0_codec, compositor=comp, phys_rank=rank, phys_world=world,
                                 fused=not args.no_fuse, coll=coll, main_stream=stream)
@@ -737,7 +772,7 @@ def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, s
                 + (" [collectives: " + ("library RCCL on the trace stream" if (tg is not None and tg.coll is not None)
                                         else "torch.distributed") + "]")
                 + (" (one gather per frame)" if args.no_pipeline else
-                   f" ({args.batch} frames per gather, {args.band_format} bands, double-buffered: the gather of "
+                   f" ({tg.F if tg is not None else args.batch} frames per gather, {args.band_format} bands, double-buffered: the gather of "
                    f"one batch overlaps the trace of the next)"),
                 "rays_per_frame": rays_per_frame,
             },
