@@ -56,9 +56,10 @@ def parse(argv=None):
                     help="N>1: comma list of further configs run through the same band pipeline after --config and "
                          "reported under 'also' (default C5: 7680x4320, the config BASELINE names for the 1/2/4/8-GPU "
                          "scaling curve); '' = none")
-    ap.add_argument("--also", default="C3",
+    ap.add_argument("--also", default="C3,C5",
                     help="N=1: comma list of further configs measured in the same run and reported under 'also' "
-                         "(default C3, the north-star config: depth 4, 2 lights); '' = none")
+                         "(default C3, the north-star config: depth 4, 2 lights, and C5, the 7680x4320 config of "
+                         "BASELINE's 1/2/4/8-GPU curve -- the N > 1 lines carry it as also.C5); '' = none")
     ap.add_argument("--size", default="",
                     help="WxH: probe runs only -- the config's scene at another frame size (never the bench line)")
     ap.add_argument("--band-rows", type=int, default=8)
