@@ -34,8 +34,10 @@ def main():
     ap.add_argument("--configs", nargs="+", default=["C2", "C3", "C4", "C5"])
     ap.add_argument("--slots-lib", default=os.path.join(ROOT, "uu-infogr-raytracer_amd/lib/ab/libraytracer_hip_slots.so"))
     ap.add_argument("--slots2-lib", default=os.path.join(ROOT, "uu-infogr-raytracer_amd/lib/ab/libraytracer_hip_slots2.so"))
+    ap.add_argument("--base-lib", default=os.path.join(ROOT, "uu-infogr-raytracer_amd/lib/libraytracer_hip.so"),
+                    help="the timed build whose executed (useful) tests are counted")
     a = ap.parse_args()
-    base = counts(os.path.join(ROOT, "uu-infogr-raytracer_amd/lib/libraytracer_hip.so"), a.configs)
+    base = counts(a.base_lib, a.configs)
     slots = counts(a.slots_lib, a.configs)
     slots2 = counts(a.slots2_lib, a.configs)
     for n in a.configs:
