@@ -550,7 +550,16 @@ def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, s
                 # (~20 us each, profiles/r03_dist_stages.txt).  Pipelined runs keep torch.distributed on
                 # side streams, where the gather of batch b-1 overlaps the trace of batch b.
                 from raytracer_hip.dist import LibraryCollectives
-                coll = LibraryCollectives(ctx, rank, world, lambda t: dist.broadcast(t, src=0))
+                try:
+                    coll = LibraryCollectives(ctx, rank, world, lambda t: dist.broadcast(t, src=0))
+                except Exception as e:  # e.g. no loadable librccl: every rank fails alike, before any init
+                    print(f"[rank {rank}] library communicator unavailable ({e}); torch.distributed collectives",
+                          file=sys.stderr, flush=True)
+                    coll = None
+                ok = torch.tensor([1 if coll is not None else 0], dtype=torch.int32, device="cuda")
+                dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # one choice for every rank
+                if int(ok.item()) == 0:
+                    coll = None
             tg = TileBandGather(rb, torch.device("cuda", local), batch,
                                 lambda n: wire_layout(W, H, rb.band_rows, band_world, n), t_encode, t_decode,
                                 rank0_codec=args.rank0_codec, compositor=comp, phys_rank=rank, phys_world=world,
