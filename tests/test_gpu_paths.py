@@ -181,3 +181,33 @@ def test_bench_multi_rank_rehearsal(world, extra):
     import json
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
     assert line["n_gpus"] == world and line["verified_frames"] >= 16 and "rehearsal" in line
+
+
+QUEUE_LIB = os.path.join(ROOT, "uu-infogr-raytracer_amd", "lib", "ab", "libraytracer_hip_queue.so")
+
+
+@pytest.mark.skipif(not os.path.exists(QUEUE_LIB), reason="shadow-queue build absent "
+                    "(make -C uu-infogr-raytracer_amd/csrc variant NAME=queue VFLAGS=-DRT_SHADOW_QUEUE=1)")
+def test_shadow_queue_build_matches_goldens(golden):
+    """The bundle kernel's shadow-queue compaction (RT_SHADOW_QUEUE=1: measured, off by default,
+    profiles/ab/r03_shadow_queue_rejected.txt) renders the full-size C4 and C5 goldens bit for bit.
+    One child process loads that build (RAYTRACER_HIP_LIB) and prints each frame's CRC."""
+    code = ("import sys, json, zlib; sys.path.insert(0, %r)\n"
+            "from raytracer_hip import Context, scenes\n"
+            "import torch\n"
+            "out = {}\n"
+            "with Context(1) as c:\n"
+            "    for n in ('C4', 'C5'):\n"
+            "        sc = scenes.config(n); c.set_scene(sc)\n"
+            "        f = torch.empty(sc.width * sc.height, dtype=torch.int32, device='cuda')\n"
+            "        c.render_device(sc.width, sc.height, f.data_ptr(), torch.cuda.current_stream().cuda_stream)\n"
+            "        torch.cuda.synchronize()\n"
+            "        out[n] = '%%08x' %% (zlib.crc32(f.cpu().numpy().tobytes()) & 0xFFFFFFFF)\n"
+            "print(json.dumps(out))\n") % os.path.join(ROOT, "uu-infogr-raytracer_amd")
+    env = dict(os.environ, RAYTRACER_HIP_LIB=QUEUE_LIB)
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=110, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    import json
+    got = json.loads(r.stdout.strip().splitlines()[-1])
+    for n in ("C4", "C5"):
+        assert got[n] == golden["cases"][n]["crc32"], n
