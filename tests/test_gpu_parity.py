@@ -84,6 +84,26 @@ def test_dense_random_scenes_vs_oracle(gpu_ctx, oracle, seed):
     assert ray_counts(st) == {k: ost[k] for k in ("primary_rays", "reflect_rays", "shadow_rays")}
 
 
+@pytest.mark.parametrize("n_lights", [1, 4, 5, 8])
+@pytest.mark.parametrize("limit", [0, 5, 7, 9])
+def test_bundle_light_counts_and_stacks(gpu_ctx, oracle, n_lights, limit):
+    """The bundle kernel on either side of the merged shadow pass's bound (L <= 4 lights: one loop
+    over the union of the lights' candidates; L = 5, 8: a pass per light) and across its stacks
+    (limit 0 / 5 / 7: the LDS stack with K = 1 / 6 / 8; limit 9: the scratch stack), with mirror
+    chains: every pixel and ray count against the oracle."""
+    import random_scenes
+    base = random_scenes.random_scene(100 + 7 * n_lights + limit, 128, 96, dense=True)
+    rng = np.random.default_rng(1000 * n_lights + limit)
+    lights = [scenes.Light(tuple(float(np.float32(x)) for x in rng.uniform(-30, 30, 3)),
+                           float(np.float32(rng.uniform(0.2, 1.2)))) for _ in range(n_lights)]
+    sc = scenes.Scene(f"bundle_L{n_lights}_lim{limit}", 128, 96, base.spheres, base.planes, lights, base.ambient,
+                      limit, base.camera)
+    px, st = render_gpu(gpu_ctx, sc)
+    want, ost = oracle.render(sc, oracle.MODE_NEAREST, 8)
+    assert_same(px, want, sc.name)
+    assert ray_counts(st) == {k: ost[k] for k in ("primary_rays", "reflect_rays", "shadow_rays")}
+
+
 @pytest.mark.parametrize("n_lights", [3000, 4200])
 def test_many_lights_with_and_without_the_shadow_cull_table(gpu_ctx, oracle, n_lights):
     """The bundle kernel's shadow culling reads the sphere centres pre-projected into each light's
