@@ -345,6 +345,12 @@ class TileBandGather:
         # reader=b, the receive buffer's last reader -- waits on); ring_of refuses provisional batches.
         self.provisional = set()
         self.decodes_of = {}    # batch -> decodes issued (2 for a redone speculative batch)
+        # defer_checks (GPUs; a run of at most three batches): a speculative batch's reduced size is read
+        # back asynchronously instead of behind a host wait in the middle of the run, and the caller
+        # checks it after its own synchronisation (check_deferred); a batch that outgrew its gather
+        # then stays provisional and the caller repeats the run without speculation
+        self.defer_checks = False
+        self.pending_checks = []  # [(batch, n_frames, speculative bytes, size slot)]
 
     def set_capacity(self, margin=1.25):
         """From now on gather each batch with a speculative size -- `margin` x the largest wire per
@@ -517,6 +523,17 @@ class TileBandGather:
             if decode_first:  # (a wire cut short decodes stale payload bytes inside its own slot)
                 self.provisional.add(b)
                 self._decode(b, n_frames, gw)
+            if decode_first and self.defer_checks and self.cuda:
+                import torch
+                i = b % 3
+                with torch.cuda.stream(self.comm):  # after the size reduce, no host wait
+                    work.wait()
+                    self.size_host[i:i + 1].copy_(self.size[i], non_blocking=True)
+                self.pending_checks.append((b, n_frames, n_spec, i))
+                self.bytes_sent += n_spec
+                if self.root:
+                    self.decoded += 1
+                return
             n = self._read_size(b % 3, work)
             self.max_per_frame = max(self.max_per_frame, n / n_frames)
             self.bytes_sent += n_spec
@@ -529,6 +546,23 @@ class TileBandGather:
             self.provisional.discard(b)  # the decode that stands has been issued
         if self.root:
             self.decoded += 1
+
+    def check_deferred(self):
+        """After the caller's device synchronisation: the deferred size checks (defer_checks).  Returns
+        True when every speculative gather sufficed (the batches are final); False when some wire
+        outgrew its gather (every rank sees the same reduced size, so every rank returns the same) --
+        those batches stay provisional and the run must be repeated without speculation."""
+        ok = True
+        for b, n_frames, n_spec, i in self.pending_checks:
+            n = (int(self.size_host[i]) + 7) // 8 * 8
+            self.max_per_frame = max(self.max_per_frame, n / n_frames)
+            if n > n_spec:
+                ok = False
+                self.redone += 1
+            else:
+                self.provisional.discard(b)
+        self.pending_checks = []
+        return ok
 
     def _decode(self, b, n_frames, gw):
         """Rank 0: after gather `gw`, decode batch b's wires into frame ring b % 3 (on `dec`).  A
