@@ -166,3 +166,24 @@ def test_gloo_tile_encoded_gather(tmp_path, world, frames, per_batch, rank0_code
             p.kill()
     assert codes == [0] * world, codes
     assert result.read_text() == "ok"
+
+
+def test_deferred_size_check_decision():
+    """TileBandGather.check_deferred (the one-batch bench run's size check after its closing sync):
+    a speculative gather that sufficed makes its batch final; one that a wire outgrew keeps the batch
+    provisional (ring_of refuses it) and asks the caller to repeat the run."""
+    from raytracer_hip import tilecodec
+    from raytracer_hip.dist import TileBandGather
+    W, H, br = 64, 32, 8
+    rb = RowBands(W, H, br, 0, 1)
+    g = TileBandGather(rb, "cpu", 4, lambda n: tilecodec.layout(W, H, br, 1, n), None, None, rank0_codec=True)
+    g.provisional.update({0, 1})
+    g.pending_checks = [(0, 4, 800, 0)]
+    g.size_host[0] = 790  # rounded up to 792 <= 800: the gather sufficed
+    assert g.check_deferred() is True and 0 not in g.provisional and g.redone == 0
+    g.pending_checks = [(1, 4, 800, 1)]
+    g.size_host[1] = 801
+    assert g.check_deferred() is False and 1 in g.provisional and g.redone == 1
+    assert g.pending_checks == [] and g.max_per_frame == 808 / 4
+    with pytest.raises(RuntimeError):
+        g.ring_of(1)
