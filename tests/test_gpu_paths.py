@@ -154,8 +154,8 @@ def test_tile_pipeline_on_cuda_streams(extra, shape):
     size = {"small": ["--size", "640x360", "--steps", "40", "--warmup", "16", "--batch", "8"],
             "full": ["--steps", "300", "--warmup", "64"],
             "short": ["--steps", "20", "--warmup", "5"]}[shape]
-    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--dist-path", "--config", "C2", "--verify",
-           "--no-cpu-baseline"] + size + extra
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--dist-path", "--config", "C2",
+           "--no-cpu-baseline"] + size + extra  # (frames verified by default on the N > 1 path)
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-2000:]
     import json
@@ -175,7 +175,7 @@ def test_bench_multi_rank_rehearsal(world, extra):
         env.pop(k, None)
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--rehearse-gloo",
            "--master-port", str(_free_port()), "--config", "C3", "--size", "640x360", "--steps", "48", "--warmup", "16",
-           "--batch", "8", "--verify", "--no-cpu-baseline"] + extra
+           "--batch", "8", "--no-cpu-baseline"] + extra  # (frames verified by default at N > 1)
     r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
     assert r.returncode == 0, r.stderr[-2000:]
     import json
@@ -183,31 +183,28 @@ def test_bench_multi_rank_rehearsal(world, extra):
     assert line["n_gpus"] == world and line["verified_frames"] >= 16 and "rehearsal" in line
 
 
-QUEUE_LIB = os.path.join(ROOT, "uu-infogr-raytracer_amd", "lib", "ab", "libraytracer_hip_queue.so")
-
-
-@pytest.mark.skipif(not os.path.exists(QUEUE_LIB), reason="shadow-queue build absent "
-                    "(make -C uu-infogr-raytracer_amd/csrc variant NAME=queue VFLAGS=-DRT_SHADOW_QUEUE=1)")
-def test_shadow_queue_build_matches_goldens(golden):
-    """The bundle kernel's shadow-queue compaction (RT_SHADOW_QUEUE=1: measured, off by default,
-    profiles/ab/r03_shadow_queue_rejected.txt) renders the full-size C4 and C5 goldens bit for bit.
-    One child process loads that build (RAYTRACER_HIP_LIB) and prints each frame's CRC."""
-    code = ("import sys, json, zlib; sys.path.insert(0, %r)\n"
-            "from raytracer_hip import Context, scenes\n"
-            "import torch\n"
-            "out = {}\n"
-            "with Context(1) as c:\n"
-            "    for n in ('C4', 'C5'):\n"
-            "        sc = scenes.config(n); c.set_scene(sc)\n"
-            "        f = torch.empty(sc.width * sc.height, dtype=torch.int32, device='cuda')\n"
-            "        c.render_device(sc.width, sc.height, f.data_ptr(), torch.cuda.current_stream().cuda_stream)\n"
-            "        torch.cuda.synchronize()\n"
-            "        out[n] = '%%08x' %% (zlib.crc32(f.cpu().numpy().tobytes()) & 0xFFFFFFFF)\n"
-            "print(json.dumps(out))\n") % os.path.join(ROOT, "uu-infogr-raytracer_amd")
-    env = dict(os.environ, RAYTRACER_HIP_LIB=QUEUE_LIB)
-    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=110, env=env)
-    assert r.returncode == 0, r.stderr[-2000:]
+def test_driver_shape_forced_repeat_counts_one_attempt():
+    """The driver's N > 1 shape (20 frames, one batch, speculative gather with the size check
+    deferred past the timed region) with the speculative size forced too short (--spec-margin 0.5):
+    the timed region is repeated with exact sizes, and the line reports that attempt alone -- the
+    same rays per frame and wire bytes per frame as an unforced run (the counters of
+    both attempts were summed) -- with every frame verified (the default at N > 1)."""
     import json
-    got = json.loads(r.stdout.strip().splitlines()[-1])
-    for n in ("C4", "C5"):
-        assert got[n] == golden["cases"][n]["crc32"], n
+    lines = []
+    for margin in ("1.25", "0.5"):
+        env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
+        env.pop("WORLD_SIZE", None)
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--dist-path", "--config", "C2", "--steps", "20",
+               "--warmup", "5", "--no-cpu-baseline", "--also-dist", "", "--spec-margin", margin]
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
+        assert r.returncode == 0, r.stderr[-2000:]
+        lines.append(json.loads(r.stdout.strip().splitlines()[-1]))
+    plain, forced = lines
+    assert plain["config"]["timed_region_repeats"] == 0 and forced["config"]["timed_region_repeats"] == 1
+    assert plain["verified_frames"] == forced["verified_frames"] == 20
+    assert forced["config"]["rays_per_frame"] == plain["config"]["rays_per_frame"]
+    # wire bytes moved: the plain run gathers its speculative size (1.25 x the warm-up's wire), the
+    # repeat the exact size -- once, not added to the first attempt's
+    fb, pb = forced["config"]["gather_wire_bytes_per_frame"], plain["config"]["gather_wire_bytes_per_frame"]
+    assert 0 < fb < pb <= 1.26 * fb
+    assert forced["config"]["gather_redone_batches"] == 0

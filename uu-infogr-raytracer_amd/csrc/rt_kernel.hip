@@ -1196,91 +1196,6 @@ __device__ __forceinline__ unsigned shadow_merged(const LaunchParams& p, unsigne
     return blk;
 }
 
-// Shadow queue (bundle kernel, records up to 8 levels, S <= 64, 1 <= L <= SHADOW_MERGE_L): the
-// north star's wave ballot/prefix compaction of the shadow work.  Shading level by level leaves
-// every lane whose walk ended above a level idle through that level's shadow loop (C4: 60 M of
-// the 186 M shadow-test lane slots per frame, profiles/r03_shadow_slots.txt 'no record').  Instead,
-// each diffuse record's hit point joins a per-wave queue the moment the forward walk finds it: a
-// lane's new item goes to queue position len + (its rank among the new items, mbcnt of the
-// ballot), moved there by one ds_permute per component (the lanes without a new item take the
-// positions behind, so the 64 destinations form a permutation).  Whenever 64 items are queued they
-// are resolved as one dense chunk -- shadow_merged over the chunk's own ShadowSphere bound -- and
-// the walk's end flushes the rest.  Each item's blocked bits go back to its owner lane through LDS
-// (one word per lane: bit 4 * level + light), where the fold reads them instead of running a shadow
-// pass per level.  Outcomes are shadow_blocked's bits for the same hit point (the forward walk's
-// hp is the fold's, reflect_at), so the pixels are unchanged; only the grouping of the tests moves.
-// Measured (profiles/ab/r03_shadow_queue_rejected.txt, bit-exact): lane-slot use C4 0.596 -> 0.719,
-// C5 0.638 -> 0.740, but C4 +1.5 %, C5 +3.5 % wall -- mixed-level chunks cull worse, and the exact
-// tests it packs are the cheap part of the pass.  Off by default; RT_SHADOW_QUEUE=1 builds it.
-#ifndef RT_SHADOW_QUEUE
-#define RT_SHADOW_QUEUE 0
-#endif
-struct ShadowQueue {
-    f3 hp;        // lane j: queued item j (j < len): hit point
-    int tag = 0;  //   and owner lane | level << 6
-    int len = 0;  // items queued (wave-uniform, < 64 between steps)
-};
-
-// Resolves the n (1..64) items held by lanes 0..n-1 and ORs their blocked bits into res[owner].
-template <typename T>
-__device__ __forceinline__ void shadow_chunk(const LaunchParams& p, f3 hp, int tag, int n, unsigned* res, T& tl) {
-    const int lane = threadIdx.x & 63;
-    const bool v = lane < n;
-    if (n < 64) {  // idle lanes carry a copy of lane 0's item (same branches, results dropped)
-        const f3 r = readlane3(hp, 0);
-        if (!v) hp = r;
-    }
-    const unsigned want = v ? (1u << p.L) - 1u : 0u;
-    // (a bound per fold level present in the chunk instead: -5 M slots, no faster -- r03_shadow_queue_rejected.txt)
-    const unsigned memb = shadow_members(p, make_shadow_sphere(hp, v), want);
-    const unsigned blk = shadow_merged(p, memb, hp, want, v, v, tl);
-    if (v && blk != 0u)
-        __hip_atomic_fetch_or(&res[tag & 63], blk << ((tag >> 6) * 4), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-}
-
-// One forward-walk step of the queue (converged call): lanes with `add` append (hp, level); full
-// chunks are resolved; `flush` (the walk has ended) resolves what is left.
-template <typename T>
-__device__ __forceinline__ void shadow_queue_step(const LaunchParams& p, ShadowQueue& q, bool add, f3 hp, int level,
-                                                  bool flush, unsigned* res, T& tl) {
-    const int lane = threadIdx.x & 63;
-    const unsigned long long m = __builtin_amdgcn_ballot_w64(add);
-    const int cnt = (int)__builtin_popcountll(m);
-    f3 r = mk(0.0f, 0.0f, 0.0f);
-    int rt = 0;
-    bool second = false;
-    if (cnt > 0) {  // wave-uniform
-        const unsigned long long o = ~m;
-        const int r_new = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-        const int r_old = (int)__builtin_amdgcn_mbcnt_hi((unsigned)(o >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)o, 0u));
-        const int dst = ((q.len + (add ? r_new : cnt + r_old)) & 63) << 2;
-        r.x = __int_as_float(__builtin_amdgcn_ds_permute(dst, __float_as_int(hp.x)));
-        r.y = __int_as_float(__builtin_amdgcn_ds_permute(dst, __float_as_int(hp.y)));
-        r.z = __int_as_float(__builtin_amdgcn_ds_permute(dst, __float_as_int(hp.z)));
-        rt = __builtin_amdgcn_ds_permute(dst, lane | (level << 6));
-        const bool got = ((lane - q.len) & 63) < cnt;  // this lane received new item (lane - len) mod 64
-        const bool first = got && lane >= q.len;        // positions len..63 of the current chunk
-        second = got && lane < q.len;                   // positions 64.. (wrapped to lanes 0..)
-        q.hp = first ? r : q.hp;
-        q.tag = first ? rt : q.tag;
-    }
-    int total = q.len + cnt;  // < 128
-    bool wrapped = total > 64;
-    int n = total >= 64 ? 64 : (flush ? total : 0);
-    while (n > 0) {  // one call site: a full chunk, then (flushing) the wrapped rest
-        shadow_chunk(p, q.hp, q.tag, n, res, tl);
-        total -= n;
-        n = 0;
-        if (wrapped) {
-            q.hp = second ? r : q.hp;
-            q.tag = second ? rt : q.tag;
-            wrapped = false;
-            n = flush ? total : 0;
-        }
-    }
-    q.len = total;
-}
-
 // Shading of one shaded hit per active lane (TraceSphere :847-873 / TracePlane :736-778),
 // converged call: the colour is accumulated in the reference's order -- mirror term (from
 // the deeper segment `sec`), then each light in order, then ambient.  Inactive lanes
@@ -1288,9 +1203,8 @@ __device__ __forceinline__ void shadow_queue_step(const LaunchParams& p, ShadowQ
 // need them form one bundle per light (common direction = the light position).
 template <bool GPOW, typename T>
 __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool is_sphere, int prim, f3 hp, f3 d, float t,
-                                           f3 sec, unsigned* n_shadow, T& tl, int qblk = -1) {
+                                           f3 sec, unsigned* n_shadow, T& tl) {
     // idle lanes (act false) carry a copy of an active lane's record: same branches, result dropped
-    // qblk >= 0 (wave-uniform choice): the record's blocked bits, resolved by the shadow queue
     const DevMaterial& m = p.mat[is_sphere ? prim : p.S + prim];
     const uint32_t flags = m.flags;
     const bool diff = act && (flags & MAT_DIFFUSE) != 0;
@@ -1299,11 +1213,9 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
     // is resolved (a superset of the shading's `need`); a cheap back-facing filter that skipped
     // some of them measured slower (C4 420 vs 401 us: its arithmetic on every lane of every level
     // cost more than the tests it saved, profiles/ab/r03_shadow_merged.txt).
-    const bool queued = qblk >= 0;
-    const bool merged =
-        !queued && p.S <= 64 && p.L >= 1 && p.L <= SHADOW_MERGE_L && __builtin_amdgcn_ballot_w64(diff) != 0;
-    unsigned blk = queued ? (unsigned)qblk : 0u;
-    if (merged || queued)
+    const bool merged = p.S <= 64 && p.L >= 1 && p.L <= SHADOW_MERGE_L && __builtin_amdgcn_ballot_w64(diff) != 0;
+    unsigned blk = 0u;
+    if (merged)
         for (int li = 0; li < p.L; ++li) tl.shadow(diff);  // (diagnostic tally of the rays resolved)
     if (merged) {
         const unsigned want = diff ? (1u << p.L) - 1u : 0u;
@@ -1330,7 +1242,7 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
         const float att = is_sphere ? cr_rcp(t) * t : (float)(1.0 / ((double)t * (double)t));
         const f3 kd = mk(m.kd[0], m.kd[1], m.kd[2]);
         ShadowSphere SS{};
-        if (!merged && !queued) SS = make_shadow_sphere(hp, diff);  // one bound for every light's shadow rays
+        if (!merged) SS = make_shadow_sphere(hp, diff);  // one bound for every light's shadow rays
         unsigned long long umask = 0;  // (diagnostic builds: the union of the lights' candidates)
         for (int li = 0; li < p.L; ++li) {
             const DevLight& l = p.li[li];
@@ -1347,8 +1259,8 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
             }
             ph = add(ph, spec);
             const bool need = diff && shadow_matters(ph, l.intensity, att);
-            bool blocked = (merged || queued) ? ((blk >> li) & 1u) != 0 : !need;
-            if (!merged && !queued && __builtin_amdgcn_ballot_w64(need) != 0) {  // some lane's pixel depends on this test
+            bool blocked = merged ? ((blk >> li) & 1u) != 0 : !need;
+            if (!merged && __builtin_amdgcn_ballot_w64(need) != 0) {  // some lane's pixel depends on this test
                 tl.shadow(need);
                 const f3 hs = need ? hp : SS.O;  // idle lanes mirror a shading lane (results ignored)
                 for (int base = 0; base < p.S; base += 64) {
@@ -1397,8 +1309,7 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
 // hit is shaded; a mirror hit consumes the colour of the segment after it (levels 0..limit push
 // at most one record each, so K = limit + 1 records suffice).  Returns the lane's colour.
 template <bool GPOW, typename STK, typename T>
-__device__ __forceinline__ f3 fold_converged(const LaunchParams& p, STK& stk, f3 leaf, unsigned* cnt, T& tl,
-                                             const unsigned* qres = nullptr) {
+__device__ __forceinline__ f3 fold_converged(const LaunchParams& p, STK& stk, f3 leaf, unsigned* cnt, T& tl) {
     f3 col = leaf;
     const int depth = stk.n;
     int level = (int)wave_max((float)depth);
@@ -1421,18 +1332,17 @@ __device__ __forceinline__ f3 fold_converged(const LaunchParams& p, STK& stk, f3
         const int code = __float_as_int(rb.w);
         const bool is_s = code >= 0;
         tl.set_level(level);
-        const int qblk = qres ? (int)((qres[threadIdx.x & 63] >> (level * 4)) & 0xFu) : -1;  // (shadow queue)
         col = shade_bundle<GPOW>(p, act, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z), ra.w,
-                                 col, cnt, tl, qblk);
+                                 col, cnt, tl);
     }
     return col;
 }
 
 // BUNDLE kernel (scenes with >= CULL_MIN_SPHERES spheres): converged control flow so that
 // every segment and every light can form a wave bundle and cull the sphere list.
-template <int K, bool GPOW, bool TILES, bool Q, typename T>
+template <int K, bool GPOW, bool TILES, typename T>
 __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int tile_x, float2* stk_lv, float* stk_dv,
-                                                      unsigned* qres, T& tl) {
+                                                      T& tl) {
     const int lane = threadIdx.x & 63;
     const TilePixel tpx = tile_pixel(p, tile_x * TILE_W + (lane & 7), blockIdx.y * TILE_H + (lane >> 3));
     const int x = tpx.x, y = tpx.y;
@@ -1457,15 +1367,7 @@ __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int
     bool active = valid;
     const unsigned long long pmask = p.prim_const ? prim_box_mask(p, x, y) : 0;
     Hit h = nearest_bundle<true>(p, o, d, active, tl, pmask);
-    // shadow queue (wave-uniform): records of at most 8 levels (4 bits each in the lane's LDS word)
-    // (Q: the host launches the queue instantiation only for S <= 64, 1 <= L <= SHADOW_MERGE_L)
-    constexpr bool queue = Q && K <= 8;
-    ShadowQueue q;
-    if (queue) qres[threadIdx.x & 63] = 0u;
     for (int count = 0;; ++count) {
-        bool enq = false;  // a diffuse record pushed at this step (shadow queue)
-        f3 hq = mk(0.0f, 0.0f, 0.0f);
-        const int level = stk.n;
         if (active) {
             const bool is_sphere = h.prim >= 0;
             if (h.prim == HIT_NONE || h.t - 0.01f <= 0.0f) {  // nothing hit / too close: Zero (:731, :839)
@@ -1478,8 +1380,6 @@ __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int
                 stk.push(make_float4(hp.x, hp.y, hp.z, h.t), make_float4(d.x, d.y, d.z, __int_as_float(h.prim)));
                 const int prim = is_sphere ? h.prim : ~h.prim;
                 const uint32_t flags = p.mat[is_sphere ? prim : p.S + prim].flags;
-                enq = (flags & MAT_DIFFUSE) != 0;
-                hq = hp;
                 if (!(flags & MAT_MIRROR)) {
                     active = false;
                 } else {
@@ -1488,9 +1388,7 @@ __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int
                 }
             }
         }
-        const bool done = __builtin_amdgcn_ballot_w64(active) == 0;
-        if (queue) shadow_queue_step(p, q, enq, hq, level, done, qres, tl);
-        if (done) break;
+        if (__builtin_amdgcn_ballot_w64(active) == 0) break;
         if (count + 1 > p.limit) {
             // terminal segment (see terminal_direct): only lanes whose nearest plane lies beyond
             // 0.01 need the spheres; the others are Zero
@@ -1512,7 +1410,7 @@ __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int
         }
     }
 
-    const f3 col = fold_converged<GPOW>(p, stk, leaf, &cnt, tl, queue ? qres : nullptr);
+    const f3 col = fold_converged<GPOW>(p, stk, leaf, &cnt, tl);
     const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
     if constexpr (TILES) encode_tile_fused(p, px32, valid);
     else {
@@ -1532,29 +1430,28 @@ __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int
 // spilled to VGPR lanes) and 64 VGPRs (8 waves): C4 -2.6 %, C5 -7.5 %.  Not with GPOW (the f64
 // Math.Pow path would spill ~150 B/lane to scratch).  The direct kernel needs no cap (79 SGPRs, 48
 // VGPRs).
-template <int K, bool GPOW, bool STATS, bool TILES, bool Q>
+template <int K, bool GPOW, bool STATS, bool TILES>
 __device__ __forceinline__ void bundle_kernel_body(const LaunchParams& p) {
     constexpr int LDS_LEVELS = StackFor<K>::lds_levels;  // LdsStack slots, else unused
     __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
     __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * WG_THREADS : 1];
-    __shared__ unsigned qres[Q && K <= 8 ? WG_THREADS : 1];  // shadow queue results
     if (blockIdx.z < (unsigned)p.copy_z) {  // wave-uniform: the fused hand-off's copy slice
         copy_slice(p);
         return;
     }
     Tally<STATS> tl;
     tl.init(p);
-    const unsigned cnt = trace_tile_bundle<K, GPOW, TILES, Q>(p, blockIdx.x, stk_lv, stk_dv, qres, tl);
+    const unsigned cnt = trace_tile_bundle<K, GPOW, TILES>(p, blockIdx.x, stk_lv, stk_dv, tl);
     add_counters<STATS>(p, threadIdx.x & 63, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
 }
-template <int K, bool STATS, bool TILES, bool Q>
+template <int K, bool STATS, bool TILES>
 __global__ __launch_bounds__(WG_THREADS, 8) __attribute__((amdgpu_num_sgpr(80))) void trace_bundle_kernel(
     LaunchParams p) {
-    bundle_kernel_body<K, false, STATS, TILES, Q>(p);
+    bundle_kernel_body<K, false, STATS, TILES>(p);
 }
-template <int K, bool STATS, bool TILES, bool Q>
+template <int K, bool STATS, bool TILES>
 __global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel_gpow(LaunchParams p) {
-    bundle_kernel_body<K, true, STATS, TILES, Q>(p);
+    bundle_kernel_body<K, true, STATS, TILES>(p);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1675,13 +1572,11 @@ struct DirectK {
         static constexpr auto fn = trace_direct_kernel<K, GPOW, STATS, SMAX, TILES>;
     };
 };
-template <bool GPOW, bool STATS, bool TILES, bool Q>
+template <bool GPOW, bool STATS, bool TILES>
 struct BundleK {
     template <int K>
     struct at {
-        static constexpr bool q = Q && K <= 8;  // the shadow queue keeps 4 bits per level in one LDS word
-        static constexpr auto fn =
-            GPOW ? trace_bundle_kernel_gpow<K, STATS, TILES, q> : trace_bundle_kernel<K, STATS, TILES, q>;
+        static constexpr auto fn = GPOW ? trace_bundle_kernel_gpow<K, STATS, TILES> : trace_bundle_kernel<K, STATS, TILES>;
     };
 };
 
@@ -1691,17 +1586,7 @@ constexpr int DIRECT_SMAX = 8;
 
 template <bool GPOW, bool STATS, bool TILES = false>
 static void launch_variant(const LaunchParams& p, bool bundle, dim3 grid, dim3 block, hipStream_t s) {
-    // the shadow queue (see ShadowQueue): S <= 64 spheres and 1..SHADOW_MERGE_L lights
-    const bool queue = p.S <= 64 && p.L >= 1 && p.L <= SHADOW_MERGE_L;
-    if (bundle) {
-        if constexpr (RT_SHADOW_QUEUE) {
-            if (queue) {
-                launch_by_depth<BundleK<GPOW, STATS, TILES, true>::template at>(p, grid, block, s);
-                return;
-            }
-        }
-        launch_by_depth<BundleK<GPOW, STATS, TILES, false>::template at>(p, grid, block, s);
-    }
+    if (bundle) launch_by_depth<BundleK<GPOW, STATS, TILES>::template at>(p, grid, block, s);
     else if (p.S <= DIRECT_SMAX)
         launch_by_depth<DirectK<GPOW, STATS, DIRECT_SMAX, TILES>::template at>(p, grid, block, s);
     else launch_by_depth<DirectK<GPOW, STATS, 0, TILES>::template at>(p, grid, block, s);
