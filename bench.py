@@ -56,10 +56,11 @@ def parse(argv=None):
                     help="N>1: comma list of further configs run through the same band pipeline after --config and "
                          "reported under 'also' (default C5: 7680x4320, the config BASELINE names for the 1/2/4/8-GPU "
                          "scaling curve); '' = none")
-    ap.add_argument("--also", default="C3,C5",
+    ap.add_argument("--also", default="C3,C4,C5",
                     help="N=1: comma list of further configs measured in the same run and reported under 'also' "
-                         "(default C3, the north-star config: depth 4, 2 lights, and C5, the 7680x4320 config of "
-                         "BASELINE's 1/2/4/8-GPU curve -- the N > 1 lines carry it as also.C5); '' = none")
+                         "(default C3, the north-star config: depth 4, 2 lights; C4, 3840x2160 with 64 spheres, "
+                         "4 lights, depth 6 -- BASELINE's LDS/compaction stress config; and C5, the 7680x4320 "
+                         "config of BASELINE's 1/2/4/8-GPU curve -- the N > 1 lines carry it as also.C5); '' = none")
     ap.add_argument("--size", default="",
                     help="WxH: probe runs only -- the config's scene at another frame size (never the bench line)")
     ap.add_argument("--band-rows", type=int, default=8)
@@ -92,6 +93,9 @@ def parse(argv=None):
                     help="N>1 tiles: read every batch's reduced wire size back before its gather (default: after "
                          "the warm-up, gather at 1.25 x the largest wire per frame seen so far right behind the size "
                          "reduce, check the reduced size before decoding and gather again when it was exceeded)")
+    ap.add_argument("--spec-margin", type=float, default=1.25,
+                    help="N>1 tiles: speculative gather size = this x the warm-up's largest wire per frame (< 1: "
+                         "probe/test of the too-short path, which repeats a one-batch timed region)")
     ap.add_argument("--compositor", choices=["auto", "on", "off"], default="auto",
                     help="N>1 tiles: rank 0 traces nothing and assembles the frames that ranks 1..N-1 "
                          "trace as a band world of N-1 (auto: N >= 8, where rank 0's own share plus the "
@@ -102,9 +106,11 @@ def parse(argv=None):
                          "communicator on the trace/encode/decode stream (rt_comm_*)")
     ap.add_argument("--dist-path", action="store_true",
                     help="rehearsal: run the N>1 band/gather path even with one process (RCCL world of 1)")
-    ap.add_argument("--verify", action="store_true",
-                    help="N>1 path: after the timed run rank 0 compares every frame still in its frame rings (tiles) "
-                         "with a single-launch render of the same view; exit 3 on a mismatch")
+    ap.add_argument("--no-verify", dest="verify", action="store_false",
+                    help="N>1 path: skip the check after the timed run (default: rank 0 compares every frame still "
+                         "in its frame rings -- tiles: all frames of a run of <= 3 batches -- with a single-launch "
+                         "render of the same view, reports verified_frames, and every rank exits 3 on a mismatch)")
+    ap.add_argument("--verify", dest="verify", action="store_true", help="(the default; kept for old command lines)")
     ap.add_argument("--master-port", type=int, default=29531, help="self-launch (--gpus N > 1): rendezvous port")
     ap.add_argument("--rehearse-gloo", action="store_true",
                     help="rehearsal of the N > 1 path on fewer GPUs than ranks: the N ranks share the visible GPUs "
@@ -165,7 +171,33 @@ def cgroup_cpus():
         quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
         return None if quota == "max" else float(quota) / float(period)
     except (OSError, ValueError):
+        pass
+    try:  # cgroup v1
+        quota = int(open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us").read())
+        period = int(open("/sys/fs/cgroup/cpu/cpu.cfs_period_us").read())
+        return None if quota <= 0 else quota / period
+    except (OSError, ValueError):
         return None
+
+
+def cgroup_throttle():
+    """(nr_periods, nr_throttled, throttled_usec) of this cgroup's CPU controller (v2 cpu.stat, or v1
+    cpu/cpu.stat with throttled_time in ns), or None when neither is readable."""
+    for path, scale in (("/sys/fs/cgroup/cpu.stat", 1.0), ("/sys/fs/cgroup/cpu/cpu.stat", 1e-3)):
+        try:
+            kv = dict(line.split()[:2] for line in open(path) if len(line.split()) >= 2)
+        except OSError:
+            continue
+        usec = kv.get("throttled_usec")
+        usec = float(usec) if usec is not None else float(kv.get("throttled_time", 0)) * scale
+        return int(kv.get("nr_periods", 0)), int(kv.get("nr_throttled", 0)), usec
+    return None
+
+
+def percentiles(xs, ps=(10, 50, 90)):
+    """Nearest-rank percentiles of xs (sorted copy)."""
+    s = sorted(xs)
+    return [s[min(len(s) - 1, max(0, int(round(p / 100.0 * (len(s) - 1)))))] for p in ps]
 
 
 def cpu_baseline(samples, seconds):
@@ -188,18 +220,25 @@ def cpu_baseline(samples, seconds):
             rays_per_frame = ost["primary_rays"] + ost["reflect_rays"] + ost["shadow_rays"]
         pyoracle.render(scene.resized(scene.width, 8), pyoracle.MODE_REFERENCE, threads)  # warm-up
         times = []
-        t_start = time.perf_counter()
+        thr0, cpu0, t_start = cgroup_throttle(), os.times(), time.perf_counter()
         while True:
             t0 = time.perf_counter()
             pyoracle.render(scene, pyoracle.MODE_REFERENCE, threads)
             times.append(time.perf_counter() - t0)
             if (time.perf_counter() - t_start > seconds * share and len(times) >= 3) or len(times) >= 200:
                 break
-        times.sort()
-        med = times[len(times) // 2]
+        wall = time.perf_counter() - t_start
+        thr1, cpu1 = cgroup_throttle(), os.times()
+        p10, med, p90 = percentiles(times)
         entry = {"value": rays_per_frame / med / 1e6, "unit": "Mray/s", "fps": 1.0 / med, "frames": len(times),
                  "workload": f"{scene.name}: {scene.width}x{scene.height}, {len(scene.spheres)} spheres, "
-                             f"{len(scene.lights)} lights, depth {scene.recursion_limit + 1}"}
+                             f"{len(scene.lights)} lights, depth {scene.recursion_limit + 1}",
+                 "frame_ms_p10_p50_p90": [round(x * 1e3, 3) for x in (p10, med, p90)],
+                 # CPU time the process got per wall second: ~threads when every worker ran all the time
+                 "cpus_scheduled": round(((cpu1.user - cpu0.user) + (cpu1.system - cpu0.system)) / wall, 2),
+                 "cgroup_throttled": None if not (thr0 and thr1) else {
+                     "periods": thr1[0] - thr0[0], "nr_throttled": thr1[1] - thr0[1],
+                     "throttled_ms": round((thr1[2] - thr0[2]) / 1e3, 1)}}
         if out is None:
             out = dict(entry)
             out.update({
@@ -209,7 +248,8 @@ def cpu_baseline(samples, seconds):
                           f"restatement of RayTracer.cs (all-hit shading, per-pixel camera trig, column-outer/"
                           f"row-parallel loop), {threads} threads = every CPU this process may use "
                           f"(sched_getaffinity {affinity} CPUs, cgroup quota {quota if quota else 'none'} CPUs, "
-                          f"os.cpu_count {os.cpu_count()}) on {cpu_model()}",
+                          f"os.cpu_count {os.cpu_count()}) on {cpu_model()}; the spread: frame_ms_p10_p50_p90, "
+                          f"cpus_scheduled (process CPU time / wall) and the cgroup's throttling over the sample",
                 "others": {},
             })
         else:
@@ -550,15 +590,18 @@ def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, s
                 # (~20 us each, profiles/r03_dist_stages.txt).  Pipelined runs keep torch.distributed on
                 # side streams, where the gather of batch b-1 overlaps the trace of batch b.
                 from raytracer_hip.dist import LibraryCollectives
-                try:
-                    coll = LibraryCollectives(ctx, rank, world, lambda t: dist.broadcast(t, src=0))
-                except Exception as e:  # e.g. no loadable librccl: every rank fails alike, before any init
+
+                def agree_min(v):
+                    t = torch.tensor([v], dtype=torch.int32, device="cuda")
+                    dist.all_reduce(t, op=dist.ReduceOp.MIN)
+                    return int(t.item())
+                try:  # (collective; every decision inside is taken alike on every rank)
+                    coll = LibraryCollectives(ctx, rank, world, lambda t: dist.broadcast(t, src=0), agree_min)
+                except Exception as e:  # CommUnavailable on every rank, or rt_comm_init failed on this one
                     print(f"[rank {rank}] library communicator unavailable ({e}); torch.distributed collectives",
                           file=sys.stderr, flush=True)
                     coll = None
-                ok = torch.tensor([1 if coll is not None else 0], dtype=torch.int32, device="cuda")
-                dist.all_reduce(ok, op=dist.ReduceOp.MIN)  # one choice for every rank
-                if int(ok.item()) == 0:
+                if agree_min(1 if coll is not None else 0) == 0:  # one choice for every rank
                     coll = None
             tg = TileBandGather(rb, torch.device("cuda", local), batch,
                                 lambda n: wire_layout(W, H, rb.band_rows, band_world, n), t_encode, t_decode,
@@ -688,11 +731,8 @@ def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, s
         finish()
         torch.cuda.synchronize()
         warmup_done += launch_frames
-    ctx.reset_stats()
-    if tg is not None:
-        tg.bytes_sent = 0
-        if not args.no_speculate:
-            tg.set_capacity()  # the warm-up's largest wire per frame x 1.25 (checked per batch)
+    if tg is not None and not args.no_speculate:
+        tg.set_capacity(args.spec_margin)  # the warm-up's largest wire per frame x 1.25 (checked per batch)
 
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record(stream)  # the first record of an event creates it (~10 us of host time): not in the region
@@ -703,13 +743,8 @@ def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, s
     # final and the whole timed region is run again without speculation -- that run is reported.
     defer = (tg is not None and tg.cuda and tg.capacity_per_frame is not None and tg.F >= args.steps
              and not args.rehearse_gloo and not os.environ.get("RT_BENCH_NO_DEFER"))
-    for attempt in range(2):
-        if tg is not None:
-            tg.defer_checks = defer and attempt == 0
-            if attempt == 1:
-                tg.capacity_per_frame = None  # exact sizes: a host wait per batch, always final
-        if distributed:
-            dist.barrier()
+
+    def region():
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         ev0.record(stream)  # on the launch stream(s): the others start after it, it ends after them
@@ -722,15 +757,10 @@ def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, s
             stream.wait_stream(st_)
         ev1.record(stream)
         torch.cuda.synchronize()
-        elapsed = time.perf_counter() - t0  # this rank's time; the line reports the max over ranks
-        if distributed:
-            dist.barrier()
-        if tg is None or not tg.defer_checks or tg.check_deferred():
-            break
-        print(f"[rank {rank}] a speculative gather was too short: timed region repeated with exact sizes",
-              file=sys.stderr, flush=True)
-    if tg is not None:
-        tg.defer_checks = False
+        return time.perf_counter() - t0, host_s  # this rank's time; the line reports the max over ranks
+
+    (elapsed, host_s), repeats = timed_attempts(ctx, tg, defer, region, dist.barrier if distributed else None,
+                                                 lambda m: print(f"[rank {rank}] {m}", file=sys.stderr, flush=True))
 
     st = ctx.stats()
     rays = st["primary_rays"] + st["reflect_rays"] + st["shadow_rays"]
@@ -740,8 +770,19 @@ def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, s
     gather_info = None
     if tg is not None:
         gather_info = {"bytes_sent": tg.bytes_sent, "speculative": tg.capacity_per_frame is not None,
-                       "redone": tg.redone}
-    verified = verify_rings(ctx, tg, W, H, args.steps, torch) if (args.verify and rank == 0) else None
+                       "redone": tg.redone, "repeats": repeats}
+    verified = None
+    if args.verify:
+        # rank 0 checks the decoded frames; every rank learns the outcome (and exits alike on a mismatch)
+        verified, bad = verify_rings(ctx, tg, W, H, args.steps, torch) if rank == 0 else (0, 0)
+        if distributed:
+            flag = torch.tensor([bad], dtype=torch.int64, device="cuda")
+            dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+            bad = int(flag.item())
+        if bad:
+            print(f"[rank {rank}] verify: {sc.name} frames differ from a single-launch render", file=sys.stderr,
+                  flush=True)
+            sys.exit(3)
     # Kernel duration per launch: an untimed second pass of the same frames (same collectives on
     # every rank) with a HIP event pair around every launch on its own stream (rt_set_timing 1;
     # what rocprofv3's kernel trace reports too).  The frame period -- HIP events around the timed
@@ -849,17 +890,52 @@ def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, s
             out["config"]["gather_rgb24_bytes_per_frame"] = 3 * rb.slot_elems
             out["config"]["gather_speculative"] = gather_info["speculative"]
             out["config"]["gather_redone_batches"] = gather_info["redone"]
+            out["config"]["timed_region_repeats"] = gather_info["repeats"]
         if args.verify:
             out["verified_frames"] = verified
     ctx.close()
     return out if rank == 0 else None
 
 
+def timed_attempts(ctx, tg, defer, region, barrier=None, log=None):
+    """The N > 1 timed region, `region()` -> its timing, between two barriers.  A run of one
+    speculative batch (defer) checks its reduced wire size after the region's closing synchronisation
+    (TileBandGather.defer_checks); when the size outgrew the speculative gather (every rank sees the
+    same reduced size, so every rank decides alike) the frames are not final and the region is run
+    again with exact sizes -- that attempt is the one reported.  The library's ray/test counters and
+    the gather's byte/redo counters are reset before each attempt, so they describe the reported
+    attempt alone.  Returns (region's timing, repeats)."""
+    repeats = 0
+    timing = None
+    for attempt in range(2):
+        ctx.reset_stats()
+        if tg is not None:
+            tg.bytes_sent = 0
+            tg.redone = 0
+            tg.defer_checks = defer and attempt == 0
+            if attempt == 1:
+                tg.capacity_per_frame = None  # exact sizes: a host wait per batch, always final
+        if barrier is not None:
+            barrier()
+        timing = region()
+        if barrier is not None:
+            barrier()
+        if tg is None or not tg.defer_checks or tg.check_deferred():
+            break
+        repeats += 1
+        if log is not None:
+            log("a speculative gather was too short: timed region repeated with exact sizes")
+    if tg is not None:
+        tg.defer_checks = False
+    return timing, repeats
+
+
 def verify_rings(ctx, tg, W, H, steps, torch):
     """Rank 0 of the tile pipeline: every decoded frame left in the frame rings (the last
-    batches) must equal a single-launch render of the same view (all frames share the camera)."""
+    batches) must equal a single-launch render of the same view (all frames share the camera).
+    Returns (frames verified, 1 if one differed else 0)."""
     if tg is None or tg.frames is None:
-        return 0
+        return 0, 0
     want = torch.empty(W * H, dtype=torch.int32, device="cuda")
     ctx.render_device(W, H, want.data_ptr(), torch.cuda.current_stream().cuda_stream)
     torch.cuda.synchronize()
@@ -872,9 +948,9 @@ def verify_rings(ctx, tg, W, H, steps, torch):
             if not torch.equal(ring[f], want):
                 bad = int((ring[f] != want).sum())
                 print(f"verify: batch {b} frame {f}: {bad} pixels differ", file=sys.stderr, flush=True)
-                sys.exit(3)
+                return n, 1
             n += 1
-    return n
+    return n, 0
 
 
 def main_single(args, torch, Context, abi, scenes):

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 7
+#define RT_ABI_VERSION 8
 
 /* ---- status codes ---------------------------------------------------------- */
 enum {
@@ -291,6 +291,11 @@ int rt_finish_wire(rt_ctx* ctx, int width, int height, int band_rows, int rank, 
  *   rank 0: rt_comm_unique_id(id); share the RT_COMM_ID_BYTES with every rank (e.g. a broadcast);
  *   every rank: rt_comm_init(ctx, world, rank, id)          -- collective, on ctx's device. */
 #define RT_COMM_ID_BYTES 128
+/* (ABI 8) RT_OK when a librccl with every symbol the rt_comm_* calls use can be loaded in this
+ * process; no communicator, socket or thread is created.  Ranks agree on the result (e.g. an
+ * all_reduce(MIN)) before any of them starts rt_comm_init, which is collective: a rank that could
+ * not join would leave the others blocked inside it. */
+int rt_comm_probe(void);
 int rt_comm_unique_id(void* out_id);
 int rt_comm_init(rt_ctx* ctx, int world, int rank, const void* id);
 /* In place, count int64 values on the device: every rank ends with the element-wise maximum. */

@@ -254,3 +254,123 @@ def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batc
         dist.barrier()
     finally:
         dist.destroy_process_group()
+
+
+def run_timed_attempts(rank, world, port, result_path):
+    """bench.timed_attempts at world `world` over gloo with a speculative gather forced too short
+    (the all-reduced wire size exceeds the speculative size on every rank, as a margin below 1
+    makes it): every rank repeats the region once, and the counters afterwards (rays, wire bytes,
+    redone batches) are those of the reported, second attempt alone."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path[:0] = [root, os.path.join(root, "uu-infogr-raytracer_amd"), here]
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    from raytracer_hip import tilecodec
+    from raytracer_hip.dist import RowBands, TileBandGather
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        W, H, br, steps = 64, 32, 8, 4
+        rb = RowBands(W, H, br, rank, world)
+        tg = TileBandGather(rb, "cpu", steps, lambda n: tilecodec.layout(W, H, br, world, n), None, None,
+                            rank0_codec=True)
+        tg.capacity_per_frame = 150.0  # speculative gather: 600 bytes for the 4-frame batch
+
+        class Ctx:
+            rays = 0
+
+            def reset_stats(self):
+                self.rays = 0
+
+        ctx = Ctx()
+        rays_per_attempt = 1000 * steps
+
+        def region():
+            ctx.rays += rays_per_attempt
+            size = torch.tensor([500 + 400 * rank], dtype=torch.int64)  # this rank's wire
+            dist.all_reduce(size, op=dist.ReduceOp.MAX)
+            if tg.defer_checks:  # speculative: ships 600 bytes, the size is checked afterwards
+                tg.size_host[0] = int(size)
+                tg.provisional.add(tg.batch)
+                tg.pending_checks.append((tg.batch, steps, 600, 0))
+                tg.bytes_sent += 600
+            else:  # exact size
+                tg.bytes_sent += (int(size) + 7) // 8 * 8
+            tg.batch += 1
+            return 0.5, 0.1
+
+        logs = []
+        timing, repeats = bench.timed_attempts(ctx, tg, True, region, dist.barrier, logs.append)
+        want_bytes = (500 + 400 * (world - 1) + 7) // 8 * 8
+        good = (timing == (0.5, 0.1) and repeats == 1 and ctx.rays == rays_per_attempt
+                and tg.bytes_sent == want_bytes and tg.redone == 0 and tg.deferred_failed == 1
+                and tg.abandoned == {0} and not tg.provisional and not tg.defer_checks and len(logs) == 1)
+        ok = torch.tensor([int(good)], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if rank == 0:
+            with open(result_path, "w") as f:
+                f.write("ok" if int(ok) else "mismatch")
+        assert good, (timing, repeats, ctx.rays, tg.bytes_sent, tg.redone, tg.deferred_failed, tg.abandoned)
+    finally:
+        dist.destroy_process_group()
+
+
+def run_library_collectives(rank, world, port, probe_fails, uid_fails, init_fails, result_path):
+    """LibraryCollectives' construction protocol over gloo with a stand-in context: whichever rank
+    cannot load RCCL (probe_fails) or make the id (uid_fails: rank 0), every rank reaches the same
+    collectives and takes the same decision; rt_comm_init is entered by all ranks or by none."""
+    here = os.path.dirname(os.path.abspath(__file__))
+    root = os.path.dirname(here)
+    sys.path[:0] = [os.path.join(root, "uu-infogr-raytracer_amd"), here]
+    import torch
+    import torch.distributed as dist
+
+    from raytracer_hip.dist import CommUnavailable, LibraryCollectives
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        class Ctx:
+            inits = []
+
+            def comm_probe(self):
+                return rank not in probe_fails
+
+            def comm_unique_id(self):
+                if uid_fails:
+                    raise RuntimeError("ncclGetUniqueId failed")
+                return bytes(range(128))
+
+            def comm_init(self, w, r, uid):
+                self.inits.append((w, r, uid))
+                if r in init_fails:
+                    raise RuntimeError("ncclCommInitRank failed")
+
+        def agree_min(v):
+            t = torch.tensor([v], dtype=torch.int32)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            return int(t)
+
+        ctx = Ctx()
+        outcome = "built"
+        try:
+            LibraryCollectives(ctx, rank, world, lambda t: dist.broadcast(t, src=0), agree_min, device="cpu")
+        except CommUnavailable:
+            outcome = "unavailable"
+        except RuntimeError:
+            outcome = "init-failed"
+        chosen = agree_min(1 if outcome == "built" else 0)  # bench.py's agreement afterwards
+        expect = "unavailable" if (probe_fails or uid_fails) else ("init-failed" if rank in init_fails else "built")
+        good = outcome == expect and chosen == (0 if (probe_fails or uid_fails or init_fails) else 1)
+        good = good and (ctx.inits == [] if expect == "unavailable" else ctx.inits == [(world, rank, bytes(range(128)))])
+        ok = torch.tensor([int(good)], dtype=torch.int32)
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if rank == 0:
+            with open(result_path, "w") as f:
+                f.write("ok" if int(ok) else "mismatch")
+    finally:
+        dist.destroy_process_group()

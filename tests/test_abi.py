@@ -57,7 +57,7 @@ def test_struct_layouts_match_header():
 
 
 def test_abi_version(rtlib):
-    assert rtlib.rt_abi_version() == 7 == abi.RT_ABI_VERSION  # 7: rt_comm_* collectives on the caller stream
+    assert rtlib.rt_abi_version() == 8 == abi.RT_ABI_VERSION  # 8: rt_comm_probe (7: rt_comm_* collectives)
     hdr = open(HEADER).read()
     assert re.search(r"#define RT_ABI_VERSION (\d+)", hdr).group(1) == str(abi.RT_ABI_VERSION)
 

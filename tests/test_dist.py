@@ -183,7 +183,58 @@ def test_deferred_size_check_decision():
     assert g.check_deferred() is True and 0 not in g.provisional and g.redone == 0
     g.pending_checks = [(1, 4, 800, 1)]
     g.size_host[1] = 801
-    assert g.check_deferred() is False and 1 in g.provisional and g.redone == 1
+    assert g.check_deferred() is False and 1 not in g.provisional and 1 in g.abandoned
+    assert g.redone == 0 and g.deferred_failed == 1
     assert g.pending_checks == [] and g.max_per_frame == 808 / 4
     with pytest.raises(RuntimeError):
         g.ring_of(1)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_gloo_timed_region_repeat_counts_one_attempt(tmp_path, world):
+    """bench.py's N>1 timed region with a speculative gather forced too short (every rank repeats the
+    region, as `--spec-margin` < 1 makes it on GPUs): rays, wire bytes and redone batches reported
+    afterwards are those of the repeated attempt alone, not the sum of both."""
+    import dist_worker
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    result = tmp_path / "result.txt"
+    procs = [ctx.Process(target=dist_worker.run_timed_attempts, args=(r, world, port, str(result)))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=180)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0] * world, codes
+    assert result.read_text() == "ok"
+
+
+@pytest.mark.parametrize("world,probe_fails,uid_fails,init_fails",
+                         [(2, (), False, ()), (2, (1,), False, ()), (3, (0,), False, ()), (2, (), True, ()),
+                          (3, (), False, (2,))])
+def test_gloo_library_collectives_agree(tmp_path, world, probe_fails, uid_fails, init_fails):
+    """bench.py's choice between the library's RCCL communicator and torch.distributed: a rank that
+    cannot load RCCL, or a rank 0 that cannot make the unique id, makes every rank fall back without
+    entering rt_comm_init (no rank left blocked in a collective the others skipped); an init failure
+    on one rank makes every rank fall back through the agreement afterwards."""
+    import dist_worker
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    result = tmp_path / "result.txt"
+    procs = [ctx.Process(target=dist_worker.run_library_collectives,
+                         args=(r, world, port, probe_fails, uid_fails, init_fails, str(result)))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=120)
+    codes = [p.exitcode for p in procs]
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    assert codes == [0] * world, codes
+    assert result.read_text() == "ok"

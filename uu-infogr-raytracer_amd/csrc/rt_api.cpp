@@ -39,8 +39,18 @@ struct ncclUniqueId {
 };
 // The librccl already mapped into the process (torch's, in a torch.distributed job), so that our
 // communicator and the framework's share one RCCL instance; else the first that dlopen finds.
+// Only the library itself: its basename is "librccl.so" or "librccl.so.<version>" (RCCL's net and
+// tuner plugins, e.g. librccl-net.so, also contain "librccl" but lack the nccl* entry points).
+bool is_librccl(const char* path) {
+    const char* base = std::strrchr(path, '/');
+    base = base ? base + 1 : path;
+    if (std::strncmp(base, "librccl.so", 10) != 0) return false;
+    for (const char* p = base + 10; *p; ++p)
+        if (!(*p == '.' || (*p >= '0' && *p <= '9'))) return false;
+    return true;
+}
 int find_loaded_rccl(struct dl_phdr_info* info, size_t, void* out) {
-    if (info->dlpi_name && std::strstr(info->dlpi_name, "librccl")) {
+    if (info->dlpi_name && is_librccl(info->dlpi_name)) {
         *(std::string*)out = info->dlpi_name;
         return 1;
     }
@@ -1069,6 +1079,12 @@ int rt_decode_gathered(rt_ctx* ctx, int width, int height, int band_rows, int wo
     DeviceGuard guard(d.id);
     int e = launch_decode_gathered((const unsigned char*)d_gathered, rank_stride, d_frames, g, hip_stream);
     if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "decode launch: %s", hipGetErrorString((hipError_t)e));
+    return RT_OK;
+}
+
+int rt_comm_probe(void) {
+    std::string err;
+    if (!g_rccl.load(err)) return fail(nullptr, RT_ERR_RCCL, "%s", err.c_str());
     return RT_OK;
 }
 

@@ -199,6 +199,10 @@ class Context:
                                             C.c_void_p(d_wire), C.c_void_p(d_wire_bytes or None), C.c_void_p(stream)))
 
     # -- one-process-per-GPU collectives on the caller's stream (rt_comm_*) --------------
+    def comm_probe(self) -> bool:
+        """True when RCCL can be loaded for rt_comm_* (rt_comm_probe; creates nothing)."""
+        return self.lib.rt_comm_probe() == 0
+
     def comm_unique_id(self) -> bytes:
         """A new RCCL unique id (rank 0), to be shared with every rank (rt_comm_unique_id)."""
         buf = C.create_string_buffer(abi.RT_COMM_ID_BYTES)

@@ -14,7 +14,7 @@ PKG_ROOT = os.path.dirname(_HERE)
 # RAYTRACER_HIP_LIB selects another build of the library (A/B variants under lib/ab/)
 LIB_PATH = os.environ.get("RAYTRACER_HIP_LIB") or os.path.join(PKG_ROOT, "lib", "libraytracer_hip.so")
 
-RT_ABI_VERSION = 7  # include/raytracer_hip.h
+RT_ABI_VERSION = 8  # include/raytracer_hip.h
 RT_COMM_ID_BYTES = 128
 RT_CREATE_RCCL_GATHER = 1
 RT_BANDS_INT32, RT_BANDS_RGB24, RT_BANDS_FRAME = 0, 1, 2
@@ -139,6 +139,7 @@ EXPORTS = [
                                         C.c_int, C.c_void_p, C.c_void_p]),
     ("rt_finish_wire", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p,
                                  C.c_void_p, C.c_void_p]),
+    ("rt_comm_probe", C.c_int, []),
     ("rt_comm_unique_id", C.c_int, [C.c_void_p]),
     ("rt_comm_init", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_void_p]),
     ("rt_comm_allreduce_max_i64", C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),

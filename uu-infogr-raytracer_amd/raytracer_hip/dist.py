@@ -351,6 +351,8 @@ class TileBandGather:
         # then stays provisional and the caller repeats the run without speculation
         self.defer_checks = False
         self.pending_checks = []  # [(batch, n_frames, speculative bytes, size slot)]
+        self.deferred_failed = 0  # deferred checks that failed (each made the caller repeat its run)
+        self.abandoned = set()    # batches of a failed deferred check (ring_of refuses them)
 
     def set_capacity(self, margin=1.25):
         """From now on gather each batch with a speculative size -- `margin` x the largest wire per
@@ -409,6 +411,8 @@ class TileBandGather:
     def ring_of(self, batch):
         if batch in self.provisional:
             raise RuntimeError(f"batch {batch}: decoded speculatively, its size not yet checked")
+        if batch in self.abandoned:
+            raise RuntimeError(f"batch {batch}: its speculative gather was too short (run repeated)")
         return self.frames[batch % 3]
 
     def wire_target(self, k=None):
@@ -558,9 +562,9 @@ class TileBandGather:
             self.max_per_frame = max(self.max_per_frame, n / n_frames)
             if n > n_spec:
                 ok = False
-                self.redone += 1
-            else:
-                self.provisional.discard(b)
+                self.deferred_failed += 1  # (not a redone batch: the caller repeats the whole run)
+                self.abandoned.add(b)       # never final; its ring slot is reused by later batches
+            self.provisional.discard(b)
         self.pending_checks = []
         return ok
 
@@ -617,20 +621,44 @@ class _Done:
         return None
 
 
+class CommUnavailable(RuntimeError):
+    """Every rank agreed that the library communicator cannot be built (raised on all ranks alike)."""
+
+
 class LibraryCollectives:
     """TileBandGather's two exchange steps through the HIP library's own communicator (rt_comm_*:
     RCCL on the caller's stream) instead of torch.distributed's collective stream.
 
-    Every rank builds one (collective: rank 0 makes the unique id and broadcasts it over the
-    process group `pg_broadcast(tensor)`)."""
+    Every rank builds one; construction is collective over the process group, whose
+    `broadcast(tensor)` (from rank 0) and `agree_min(int) -> int` (minimum over ranks) it uses:
+      1. every rank probes RCCL (rt_comm_probe: loads it, creates nothing) and the ranks agree on
+         the minimum -- if any rank cannot load it, every rank raises CommUnavailable;
+      2. rank 0 makes the unique id and ALWAYS broadcasts (flag byte + id; flag 0 when making the
+         id failed), so every rank reaches the same broadcast -- a flag of 0 raises CommUnavailable
+         on every rank;
+      3. rt_comm_init on every rank (collective inside RCCL).
+    Steps 1-2 make each decision from values every rank holds, so no rank enters rt_comm_init
+    while another has given up (rank 0 raising before the broadcast hung the others).
+    A failure inside rt_comm_init itself raises only on that rank; the caller agrees on the
+    outcome afterwards (bench.py all_reduces an ok flag)."""
 
-    def __init__(self, ctx, rank, world, broadcast):
+    def __init__(self, ctx, rank, world, broadcast, agree_min, device="cuda"):
         import torch
-        uid = torch.zeros(128, dtype=torch.uint8, device="cuda")
+        if agree_min(1 if ctx.comm_probe() else 0) == 0:
+            raise CommUnavailable("librccl cannot be loaded on some rank")
+        msg = torch.zeros(1 + 128, dtype=torch.uint8, device=device)
         if rank == 0:
-            uid.copy_(torch.frombuffer(bytearray(ctx.comm_unique_id()), dtype=torch.uint8))
-        broadcast(uid)
-        ctx.comm_init(world, rank, bytes(uid.cpu().numpy().tobytes()))
+            try:
+                uid = ctx.comm_unique_id()
+                msg[1:].copy_(torch.frombuffer(bytearray(uid), dtype=torch.uint8))
+                msg[0] = 1
+            except Exception:  # noqa: BLE001 -- reported to every rank through the flag
+                msg[0] = 0
+        broadcast(msg)
+        host = msg.cpu().numpy()
+        if int(host[0]) != 1:
+            raise CommUnavailable("rank 0 could not make an RCCL unique id")
+        ctx.comm_init(world, rank, bytes(host[1:].tobytes()))
         self.ctx = ctx
 
     def all_reduce_max(self, t, stream):
