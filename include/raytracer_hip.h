@@ -117,7 +117,11 @@ enum {
  * rt_reset_stats.  rays = primary + reflected segments (terminal segments included);
  * shadow_rays = shaded diffuse hits x lights.  Times are device time measured with
  * HIP events on the stream the operation runs on, for the sampled operations only (see
- * rt_set_timing): average kernel duration = kernel_ms / timed_launches. */
+ * rt_set_timing): average kernel duration = kernel_ms / timed_launches.  rt_render_async
+ * ticks hand the previous frame to its host buffer inside the next frame's launch (a copy
+ * slice ahead of the trace workgroups): that copy's share is in the launch's kernel_ms, the
+ * last frame's copy (issued by rt_wait / the next synchronous call) is not timed, and
+ * copy_ms / timed_copies count rt_render's D2H copies only. */
 typedef struct rt_stats {
     uint64_t frames;
     uint64_t pixels;

@@ -238,6 +238,131 @@ void check_shadow_threshold() {
     std::printf("shadow_threshold: %ld (n, 2a) pairs\n", checked);
 }
 
+// The per-light shadow grids (rt_set_scene -> build_shadow_grid; looked up by rt_kernel.hip
+// shadow_members_grid): for random scenes -- unit, large and huge coordinates, tiny / zero / NaN
+// radii, grazing and degenerate lights -- and hit points near sphere surfaces, on grazing shadow
+// lines, on cell and slab edges, far beyond the table's bound and non-finite, a sphere the lookup
+// leaves out of a lane's mask must never block that lane's binary32 shadow ray (the oracle's
+// IntersectsSphere(hp, light.position, sphere, 0.001f), RayTracer.cs:573-582).  The lookup below
+// repeats the device's operations (binary32 fmaf / floor / min / max).
+unsigned long long grid_lookup(const DevShadowGrid& g, const DevLight& l, const unsigned long long* grid,
+                               const unsigned long long* slab, rt_vec3 hp) {
+    const float l1 = std::fabs(hp.x) + std::fabs(hp.y) + std::fabs(hp.z);
+    const float u = std::fmaf(hp.z, l.uz, std::fmaf(hp.y, l.uy, hp.x * l.ux));
+    const float v = std::fmaf(hp.z, l.vz, std::fmaf(hp.y, l.vy, hp.x * l.vx));
+    const float a = std::fmaf(hp.z, l.az, std::fmaf(hp.y, l.ay, hp.x * l.ax));
+    const bool near = l1 <= g.bound;
+    const float xu = std::fmaf(u, g.su, g.ou), xv = std::fmaf(v, g.sv, g.ov);
+    const bool in_grid = xu >= 0.0f && xu < (float)SHGRID_N && xv >= 0.0f && xv < (float)SHGRID_N;
+    const int iu = (int)std::fmin(std::fmax(xu, 0.0f), (float)(SHGRID_N - 1));
+    const int iv = (int)std::fmin(std::fmax(xv, 0.0f), (float)(SHGRID_N - 1));
+    const unsigned long long cell = grid[iv * SHGRID_N + iu];
+    const float mg = g.far_k * l1;
+    const bool in_box = !(u < g.bu0 - mg || u > g.bu1 + mg || v < g.bv0 - mg || v > g.bv1 + mg);
+    const float af = near ? a : a - (mg - g.far_b);
+    const float xa = std::fmin(std::fmax(std::floor(std::fmaf(af, g.sa, g.oa)), -1.0f), (float)SHGRID_SLABS);
+    const unsigned long long sl = slab[(int)xa + 1];
+    const bool take = near ? in_grid : in_box;
+    return (take ? (near ? cell : ~0ull) & sl : 0ull) | g.always;
+}
+
+void check_shadow_grid() {
+    long checked = 0, culled = 0, lanes = 0, cands = 0;
+    for (int it = 0; it < 48; ++it) {
+        const float scale = it % 4 == 3 ? 1000.0f : it % 4 == 2 ? 30.0f : 1.0f;
+        const int S = 12 + (int)(next64() % 53), L = 1 + (int)(next64() % SHADOW_MERGE_L);
+        std::vector<rt_sphere> sph((size_t)S);
+        std::vector<rt_light> li((size_t)L);
+        for (int i = 0; i < S; ++i) {
+            rt_sphere& s = sph[(size_t)i];
+            s.center = v3(unif(-8, 8) * scale, unif(-1, 3) * scale, unif(2, 40) * scale);
+            s.radius = unif(0.05f, 1.5f) * scale;
+            s.material = material((int)(next64() % 5));
+        }
+        sph[1].radius = 1e-25f;  // r^2 below 2^-100: never culled
+        sph[2].radius = 0.0f;
+        if (it % 5 == 1) sph[4].radius = NAN;
+        if (it % 6 == 2) sph[5].center = v3(3e9f, 0, 0);  // |C|_1 >= 2^30: never culled
+        for (int j = 0; j < L; ++j) {
+            rt_light& l = li[(size_t)j];
+            l.position = v3(unif(-40, 40), unif(-5, 20), unif(-20, 40));
+            l.intensity = 1.0f;
+            if (j == 1 && it % 3 == 0) l.position = v3(unif(-40, 40), 1e-3f, unif(-1, 1));  // grazing
+            if (j == 2 && it % 7 == 0) l.position = v3(1e-30f, 0, 0);                      // |p|^2 < 2^-40
+            if (j == 3 && it % 4 == 1) l.position = v3(0, 3e4f, 0);
+        }
+        rt_ctx ctx;
+        const int rc = rt_set_scene(&ctx, sph.data(), S, nullptr, 0, li.data(), L, v3(0.1f, 0.1f, 0.1f), 3);
+        CHECK(rc == RT_OK, "rt_set_scene rc %d", rc);
+        const SceneLayout& lay = ctx.layout;
+        CHECK(lay.has_shg, "no shadow grid for S=%d L=%d", S, L);
+        if (!lay.has_shg) continue;
+        const unsigned char* blob = lay.host_blob.data();
+        const DevLight* dl = (const DevLight*)(blob + lay.off_li);
+        for (int j = 0; j < L; ++j) {
+            const DevShadowGrid& g = ((const DevShadowGrid*)(blob + lay.off_shg))[j];
+            const unsigned long long* grid = (const unsigned long long*)(blob + lay.off_shgrid) + (size_t)j * SHGRID_N * SHGRID_N;
+            const unsigned long long* slab = (const unsigned long long*)(blob + lay.off_shslab) + (size_t)j * (SHGRID_SLABS + 2);
+            const DevLight& l = dl[j];
+            // the light frame (double) as the host built it
+            const double U[3] = {l.ux, l.uy, l.uz}, V[3] = {l.vx, l.vy, l.vz}, A[3] = {l.ax, l.ay, l.az};
+            for (int k = 0; k < 3000; ++k) {
+                rt_vec3 hp;
+                const rt_sphere& s = sph[next64() % (size_t)S];
+                const int kind = k % 6;
+                if (kind == 0) {  // anywhere around the scene
+                    hp = v3(unif(-20, 20) * scale, unif(-3, 6) * scale, unif(-5, 60) * scale);
+                } else if (kind == 1) {  // on / just off a sphere's surface
+                    const double d[3] = {unif(-1, 1), unif(-1, 1), unif(-1, 1)};
+                    const double n = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]) + 1e-30;
+                    const double r = (double)s.radius * (1.0 + unif(-1e-3f, 1e-2f));
+                    hp = v3((float)(s.center.x + r * d[0] / n), (float)(s.center.y + r * d[1] / n),
+                            (float)(s.center.z + r * d[2] / n));
+                } else if (kind == 2 || kind == 3) {  // a shadow line grazing a sphere (u, v at ~r from it)
+                    const double ang = unif(0, 6.2831853f), rr = (double)s.radius * (1.0 + unif(-2e-3f, 2e-2f));
+                    const double ax = unif(-30, 10) * scale;  // along the axis, behind or ahead of the sphere
+                    double c[3] = {s.center.x, s.center.y, s.center.z};
+                    double q[3];
+                    for (int e = 0; e < 3; ++e)
+                        q[e] = c[e] + rr * (std::cos(ang) * U[e] + std::sin(ang) * V[e]) + ax * A[e];
+                    hp = v3((float)q[0], (float)q[1], (float)q[2]);
+                } else if (kind == 4) {  // cell / slab edges
+                    const int iu = (int)(next64() % (SHGRID_N + 2)) - 1, iv = (int)(next64() % (SHGRID_N + 2)) - 1;
+                    const double uu = g.su != 0.0f ? ((double)iu - (double)g.ou) / (double)g.su : 0.0;
+                    const double vv = g.sv != 0.0f ? ((double)iv - (double)g.ov) / (double)g.sv : 0.0;
+                    const int ia = (int)(next64() % (SHGRID_SLABS + 2)) - 1;
+                    const double aa = g.sa != 0.0f ? ((double)ia - (double)g.oa) / (double)g.sa : 0.0;
+                    double q[3];
+                    for (int e = 0; e < 3; ++e) q[e] = uu * U[e] + vv * V[e] + aa * A[e];
+                    hp = v3((float)q[0], (float)q[1], (float)q[2]);
+                } else {  // far beyond the table's bound, and non-finite
+                    const float f = std::ldexp(1.0f, (int)(next64() % 24));
+                    hp = v3(unif(-20, 20) * scale * f, unif(-3, 6) * scale, unif(-5, 60) * scale * f);
+                    if (k % 97 == 5) hp.x = NAN;
+                    if (k % 89 == 7) hp.z = INFINITY;
+                }
+                const unsigned long long m = grid_lookup(g, l, grid, slab, hp);
+                ++lanes;
+                for (int i = 0; i < S; ++i) {
+                    if ((m >> i) & 1ull) {
+                        ++cands;
+                        continue;
+                    }
+                    int col = 0;
+                    oracle_intersect_sphere(hp, li[(size_t)j].position, sph[(size_t)i].center, sph[(size_t)i].radius,
+                                            0.001f, &col);
+                    ++checked, ++culled;
+                    CHECK(!col, "scene %d light %d: sphere %d culled but blocks hp (%a, %a, %a)", it, j, i, hp.x, hp.y,
+                          hp.z);
+                }
+            }
+        }
+    }
+    std::printf("shadow_grid: %ld culled (lane, sphere) pairs checked unblocked, %.2f candidates per lane\n", culled,
+                lanes ? (double)cands / (double)lanes : 0.0);
+    (void)checked;
+}
+
 void check_library() {
     CHECK(rt_abi_version() == RT_ABI_VERSION, "ABI version");
     int n = -1;
@@ -260,6 +385,7 @@ int main() {
     check_ppm();
     check_wire_layout();
     check_shadow_threshold();
+    check_shadow_grid();
     std::printf("san_host: %d failures\n", failures);
     return failures ? 1 : 0;
 }

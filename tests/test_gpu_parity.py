@@ -104,6 +104,48 @@ def test_bundle_light_counts_and_stacks(gpu_ctx, oracle, n_lights, limit):
     assert ray_counts(st) == {k: ost[k] for k in ("primary_rays", "reflect_rays", "shadow_rays")}
 
 
+def shadow_grid_scene(seed, width=160, height=96):
+    """A C4-like scene for the merged shadow pass's per-light grids (12-64 spheres, 1-4 lights):
+    mirror-heavy materials (deep fold levels, scattered hit points), coordinates at unit, 30x and
+    1000x scale (the grid's lane bound and margins scale with the scene), grazing lights, ground
+    and back planes reaching far beyond the bound, and cameras anywhere in the scene."""
+    rng = np.random.default_rng(20_000 + seed)
+    scale = [1.0, 30.0, 1000.0][seed % 3]
+    f = lambda x: float(np.float32(x))  # noqa: E731
+    ns = int(rng.integers(12, 65))
+    mats = [scenes.Material.mirror(scenes.ONE), scenes.Material.diffuse((0.8, 0.3, 0.2)),
+            scenes.Material.plastic((0.2, 0.7, 0.3), 2.0), scenes.Material.diffuse_mirror((0.6, 0.6, 0.9), (0.5,) * 3)]
+    sph = [scenes.Sphere((f(rng.uniform(-8, 8) * scale), f(rng.uniform(-0.7, 1.0) * scale), f(rng.uniform(4, 32) * scale)),
+                         f(rng.uniform(0.25, 1.0) * scale), mats[int(rng.integers(0, 4))]) for _ in range(ns)]
+    if seed % 4 == 1:
+        sph[3] = scenes.Sphere(sph[3].center, f(1e-3 * scale), mats[1])  # tiny
+    planes = [scenes.Plane((0.0, f(-1 * scale), 0.0), (0.0, 1.0, 0.0), scenes.REF_PLANES[0].material),
+              scenes.Plane((0.0, 0.0, f(48 * scale)), (0.0, 0.0, -1.0), scenes.Material.diffuse((0.6, 0.6, 0.6)))]
+    nl = int(rng.integers(1, 5))
+    lights = [scenes.Light((f(rng.uniform(-40, 40) * scale), f(rng.uniform(0.5, 15) * scale),
+                            f(rng.uniform(-10, 40) * scale)), 1.0) for _ in range(nl)]
+    if seed % 5 == 2:
+        lights[0] = scenes.Light((f(33 * scale), f(1e-3), f(10 * scale)), 1.0)  # grazing
+    cam = ((f(rng.uniform(-3, 3) * scale), f(rng.uniform(-0.5, 2) * scale), f(rng.uniform(-4, 10) * scale)),
+           f(rng.uniform(-0.8, 0.8)), f(rng.uniform(-0.3, 0.5)))
+    return scenes.Scene(f"grid{seed}", width, height, sph, planes, lights, scenes.REF_AMBIENT,
+                        int(rng.choice([1, 3, 5, 7])), cam)
+
+
+@pytest.mark.parametrize("seed", list(range(30)))
+def test_shadow_grid_scenes_vs_oracle(gpu_ctx, oracle, seed, monkeypatch):
+    """The bundle kernel's merged shadow pass takes each lane's sphere candidates from per-light
+    grids (rt_api.cpp build_shadow_grid); RT_SHADOW_GRID=0 at rt_set_scene keeps the per-level
+    bound instead.  Both must give the oracle's pixels and ray counts."""
+    sc = shadow_grid_scene(seed)
+    want, ost = oracle.render(sc, oracle.MODE_NEAREST, 8)
+    for grid in ("1", "0"):
+        monkeypatch.setenv("RT_SHADOW_GRID", grid)
+        px, st = render_gpu(gpu_ctx, sc)
+        assert_same(px, want, f"{sc.name} RT_SHADOW_GRID={grid}")
+        assert ray_counts(st) == ray_counts(ost)
+
+
 @pytest.mark.parametrize("n_lights", [3000, 4200])
 def test_many_lights_with_and_without_the_shadow_cull_table(gpu_ctx, oracle, n_lights):
     """The bundle kernel's shadow culling reads the sphere centres pre-projected into each light's

@@ -156,7 +156,10 @@ struct Device {
 struct SceneLayout {
     int S = 0, P = 0, L = 0, limit = 0;
     size_t off_sph = 0, off_mat = 0, off_pl = 0, off_li = 0, off_cull = 0, off_shcull = 0, bytes = 0;
+    size_t off_shg = 0, off_shgrid = 0, off_shslab = 0, off_sphp = 0;
     bool has_shcull = false;
+    bool has_shg = false;  // per-light shadow grids (DevShadowGrid) for the merged shadow pass
+    std::vector<unsigned char> host_blob;  // the uploaded scene image (host tests read the tables)
     bool generic_pow = false;        // a specular material with n not in {0.5, 1, 2}
     std::vector<DevSphere> host_sph;  // for the per-frame primary constants
 };
@@ -440,7 +443,11 @@ void scene_params(const rt_ctx* ctx, const Device& d, LaunchParams& lp) {
     lp.pl = (const DevPlane*)(base + L.off_pl);
     lp.li = (const DevLight*)(base + L.off_li);
     lp.scull = (const DevSphereCull*)(base + L.off_cull);
+    lp.sphp = (const DevSpherePair*)(base + L.off_sphp);
     lp.shcull = L.has_shcull ? (const DevShadowCull*)(base + L.off_shcull) : nullptr;
+    lp.shg = L.has_shg ? (const DevShadowGrid*)(base + L.off_shg) : nullptr;
+    lp.shgrid = L.has_shg ? (const unsigned long long*)(base + L.off_shgrid) : nullptr;
+    lp.shslab = L.has_shg ? (const unsigned long long*)(base + L.off_shslab) : nullptr;
     lp.S = L.S, lp.P = L.P, lp.L = L.L, lp.limit = L.limit;
     lp.counters = d.d_counters;
 }
@@ -669,6 +676,142 @@ void rt_destroy(rt_ctx* ctx) {
     delete ctx;
 }
 
+namespace {
+// Light frame in double (the DevLight frame is its binary32 rounding).
+struct Frame3 {
+    double U[3], V[3], A[3];
+};
+
+// The lowest value x (double) that binary32 fma(x, s, o) can map to a value >= k (k integer): every
+// x_f with floor(fl(x_f * s + o)) == k satisfies x_f >= cell_lo(k, s, o), and every x_f with that
+// floor <= k - 1 satisfies x_f < cell_lo(k, s, o)... up to the allowance eps_k (a relative 2^-24 of
+// the fma result plus double rounding here, taken 4x).  s > 0.
+double cell_lo(int k, float s, float o) { return ((double)k - 0x1p-22 * (std::fabs((double)k) + 2.0) - (double)o) / (double)s; }
+double cell_hi(int k, float s, float o) {  // the highest x that can map to k (exclusive bound of k + 1)
+    return ((double)(k + 1) + 0x1p-22 * (std::fabs((double)k + 1.0) + 2.0) - (double)o) / (double)s;
+}
+float down(double v) { float f = (float)v; return (double)f > v ? std::nextafter(f, -INFINITY) : f; }
+float up(double v) { float f = (float)v; return (double)f < v ? std::nextafter(f, INFINITY) : f; }
+
+// Shadow grid of one light (DevShadowGrid; culling only -- a sphere left out of a lane's mask must
+// provably not block that lane's shadow ray in binary32).  The argument (rt_kernel.hip cull_mask):
+// IntersectsSphere yields disc < 0 when the exact line-to-centre distance D >= r (1 + 3 eps) +
+// 9.2e-4 |u| (u = hp - C), and b >= 0 when (hp - C).A >= 4 eps |u|; either makes the ray unblocked.
+// For a lane with |hp|_1 <= B: |u| <= |C|_1 + B, and its binary32 projections u_f = hp.U etc. are
+// within 2^-21 |hp|_1 <= 2^-21 B of the exact ones in the double frame (U_f rounds U to 2^-24, three
+// products and two sums round to 2^-24 each).  So, with T_j = r'_j + 2^-8 (|C_j|_1 + B) + 2^-20 B
+// (r' >= r (1 + 2^-8) from DevSphereCull): a sphere whose centre lies farther than T_j from every
+// (u, v) a lane of cell (iu, iv) can have -- the cell's interval from the device's own fma/floor
+// mapping (cell_lo/cell_hi), grown by 2^-20 B -- has D > r (1 + 3 eps) + 2^-8 |u| (a 4x margin
+// over 9.2e-4); cells outside the grid hold no such disc at all.  Axially, sphere j may be ahead of
+// slab k only if ca_j + mB_j > a_lo(k), mB_j = 2^-8 (|C_j|_1 + B) + 2^-20 B; otherwise every lane in
+// the slab has (hp - C).A >= 2^-8 (|C_j|_1 + B) >> 4 eps |u| (b >= 0).  Lanes beyond B: their own
+// margin far_k |hp|_1 (far_k = 2^-8 + 2^-20, rounded up) on the box of all discs, and the slab of
+// a_f - (far_k |hp|_1 - 2^-8 B), which raises the slab rule's margin from B to |hp|_1.  Spheres
+// without a valid record (NaN/inf, r^2 < 2^-100, |C|_1 >= 2^30) are never culled (`always`); a
+// light whose |p|^2 lies outside [2^-40, 2^40] (the analysis' range) culls nothing.
+void build_shadow_grid(const DevLight& l, const Frame3& f, const DevSphere* sph, const DevSphereCull* cull, int S,
+                       DevShadowGrid& g, unsigned long long* grid, unsigned long long* slab) {
+    std::memset(&g, 0, sizeof g);
+    std::memset(grid, 0, sizeof(unsigned long long) * SHGRID_N * SHGRID_N);
+    std::memset(slab, 0, sizeof(unsigned long long) * (SHGRID_SLABS + 2));
+    const unsigned long long all = S >= 64 ? ~0ull : ((1ull << S) - 1ull);
+    g.bu0 = g.bv0 = INFINITY, g.bu1 = g.bv1 = -INFINITY;  // empty box: every far lane outside
+    const bool light_ok = l.a >= 0x1p-40f && l.a <= 0x1p40f && l.a2 < INFINITY;
+    std::vector<double> cu(S), cv(S), ca(S), c1(S), rr(S);
+    std::vector<bool> ok(S);
+    double cmax1 = 0.0;
+    for (int j = 0; j < S; ++j) {
+        const double c[3] = {sph[j].cx, sph[j].cy, sph[j].cz};
+        c1[j] = std::fabs(c[0]) + std::fabs(c[1]) + std::fabs(c[2]);
+        rr[j] = cull[j].rr;
+        ok[j] = light_ok && std::isfinite(c1[j]) && c1[j] < 0x1p30 && std::isfinite(rr[j]) &&
+                (double)sph[j].r2 >= 0x1p-100 && rr[j] > 0.0;
+        if (!ok[j]) {
+            g.always |= 1ull << j;
+            continue;
+        }
+        cu[j] = c[0] * f.U[0] + c[1] * f.U[1] + c[2] * f.U[2];
+        cv[j] = c[0] * f.V[0] + c[1] * f.V[1] + c[2] * f.V[2];
+        ca[j] = c[0] * f.A[0] + c[1] * f.A[1] + c[2] * f.A[2];
+        cmax1 = std::max(cmax1, c1[j]);
+    }
+    if (g.always == all) {  // nothing to cull: no lane looks anything up that matters
+        g.bound = -1.0f;    // every lane "far"
+        g.far_k = 0.0f;
+        return;
+    }
+    const double B = std::min(std::max(8.0, 1.5 * cmax1), 0x1p30);
+    g.bound = down(B);
+    g.far_k = up(0x1p-8 + 0x1p-20);
+    g.far_b = down(0x1p-8 * B);
+    double ulo = INFINITY, uhi = -INFINITY, vlo = INFINITY, vhi = -INFINITY, alo = INFINITY, ahi = -INFINITY;
+    double bu0 = INFINITY, bu1 = -INFINITY, bv0 = INFINITY, bv1 = -INFINITY;
+    std::vector<double> T(S), mB(S);
+    for (int j = 0; j < S; ++j) {
+        if (!ok[j]) continue;
+        T[j] = rr[j] + 0x1p-8 * (c1[j] + B) + 0x1p-20 * B;
+        mB[j] = 0x1p-8 * (c1[j] + B) + 0x1p-20 * B;
+        ulo = std::min(ulo, cu[j] - T[j]), uhi = std::max(uhi, cu[j] + T[j]);
+        vlo = std::min(vlo, cv[j] - T[j]), vhi = std::max(vhi, cv[j] + T[j]);
+        alo = std::min(alo, ca[j] + mB[j]), ahi = std::max(ahi, ca[j] + mB[j]);
+        const double t0 = rr[j] + 0x1p-8 * c1[j];  // far lanes add their own |hp| term
+        bu0 = std::min(bu0, cu[j] - t0), bu1 = std::max(bu1, cu[j] + t0);
+        bv0 = std::min(bv0, cv[j] - t0), bv1 = std::max(bv1, cv[j] + t0);
+    }
+    g.bu0 = down(bu0), g.bu1 = up(bu1), g.bv0 = down(bv0), g.bv1 = up(bv1);
+    // grid over [lo, hi] padded by half a cell (lanes mapped outside it see no disc: checked below)
+    auto axis = [](double lo, double hi, int n, float& s, float& o) {
+        const double cs = (hi - lo) / (n - 1);  // n - 1 cells span the range, half a cell of pad each side
+        const double lo2 = lo - 0.5 * cs;
+        s = (float)(1.0 / cs);
+        o = (float)(-lo2 * (double)s);
+    };
+    axis(ulo, uhi, SHGRID_N, g.su, g.ou);
+    axis(vlo, vhi, SHGRID_N, g.sv, g.ov);
+    bool sound = g.su > 0.0f && g.sv > 0.0f && std::isfinite(g.su) && std::isfinite(g.sv) && std::isfinite(g.ou) &&
+                 std::isfinite(g.ov);
+    // a lane mapped below cell 0 / above cell N-1 lies outside every disc
+    sound = sound && cell_hi(-1, g.su, g.ou) + 0x1p-20 * B < ulo && cell_lo(SHGRID_N, g.su, g.ou) - 0x1p-20 * B > uhi &&
+            cell_hi(-1, g.sv, g.ov) + 0x1p-20 * B < vlo && cell_lo(SHGRID_N, g.sv, g.ov) - 0x1p-20 * B > vhi;
+    if (sound) {
+        for (int iv = 0; iv < SHGRID_N; ++iv) {
+            const double v0 = cell_lo(iv, g.sv, g.ov) - 0x1p-20 * B, v1 = cell_hi(iv, g.sv, g.ov) + 0x1p-20 * B;
+            for (int iu = 0; iu < SHGRID_N; ++iu) {
+                const double u0 = cell_lo(iu, g.su, g.ou) - 0x1p-20 * B, u1 = cell_hi(iu, g.su, g.ou) + 0x1p-20 * B;
+                unsigned long long m = 0;
+                for (int j = 0; j < S; ++j) {
+                    if (!ok[j]) continue;
+                    const double du = std::max(0.0, std::max(u0 - cu[j], cu[j] - u1));
+                    const double dv = std::max(0.0, std::max(v0 - cv[j], cv[j] - v1));
+                    if (du * du + dv * dv <= T[j] * T[j] * (1.0 + 0x1p-30)) m |= 1ull << j;
+                }
+                grid[iv * SHGRID_N + iu] = m;
+            }
+        }
+    } else {  // (degenerate extents) every lane takes every sphere through the far path
+        g.bound = -1.0f;
+        g.bu0 = -INFINITY, g.bu1 = INFINITY, g.bv0 = -INFINITY, g.bv1 = INFINITY;
+    }
+    // axial slabs over [alo, ahi]: entry k + 1 for slab k (-1: below the range, every sphere)
+    {
+        const double cs = std::max((ahi - alo) / SHGRID_SLABS, 1e-30);
+        g.sa = (float)(1.0 / cs);
+        g.oa = (float)(-alo * (double)g.sa);
+        const bool sa_ok = g.sa > 0.0f && std::isfinite(g.sa) && std::isfinite(g.oa);
+        slab[0] = all;
+        for (int k = 0; k <= SHGRID_SLABS; ++k) {
+            const double a_lo = sa_ok ? cell_lo(k, g.sa, g.oa) : -INFINITY;
+            unsigned long long m = 0;
+            for (int j = 0; j < S; ++j)
+                if (ok[j] && ca[j] + mB[j] > a_lo) m |= 1ull << j;
+            slab[k + 1] = m;
+        }
+        if (!sa_ok) g.sa = 0.0f, g.oa = 0.0f;  // every lane in slab 0 (= every valid sphere)
+    }
+}
+}  // namespace
+
 int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_plane* planes, int n_planes,
                  const rt_light* lights, int n_lights, rt_vec3 ambient, int recursion_limit) {
     if (!ctx) return fail(nullptr, RT_ERR_INVALID_ARG, "NULL context");
@@ -694,9 +837,18 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
     L.off_pl = al(L.off_mat + sizeof(DevMaterial) * (size_t)(n_spheres + n_planes));
     L.off_li = al(L.off_pl + sizeof(DevPlane) * (size_t)n_planes);
     L.off_cull = al(L.off_li + sizeof(DevLight) * (size_t)n_lights);
-    L.off_shcull = al(L.off_cull + sizeof(DevSphereCull) * (size_t)n_spheres);
+    L.off_sphp = al(L.off_cull + sizeof(DevSphereCull) * (size_t)n_spheres);
+    L.off_shcull = al(L.off_sphp + sizeof(DevSpherePair) * (size_t)(s_pad / 2));
     L.has_shcull = (long long)n_lights * (long long)n_spheres <= SHADOW_CULL_MAX_ENTRIES;
-    L.bytes = al(L.off_shcull + (L.has_shcull ? sizeof(DevShadowCull) * (size_t)n_lights * (size_t)n_spheres : 0)) + 256;
+    // shadow grids: the bundle kernel's merged pass only (CULL_MIN_SPHERES <= S <= 64, 1 <= L <=
+    // SHADOW_MERGE_L); RT_SHADOW_GRID=0 keeps the per-level bound (A/B and fallback tests)
+    const char* gv = std::getenv("RT_SHADOW_GRID");
+    L.has_shg = n_spheres >= CULL_MIN_SPHERES && n_spheres <= 64 && n_lights >= 1 && n_lights <= SHADOW_MERGE_L &&
+                !(gv && std::strcmp(gv, "0") == 0);
+    L.off_shg = al(L.off_shcull + (L.has_shcull ? sizeof(DevShadowCull) * (size_t)n_lights * (size_t)n_spheres : 0));
+    L.off_shgrid = al(L.off_shg + (L.has_shg ? sizeof(DevShadowGrid) * (size_t)n_lights : 0));
+    L.off_shslab = al(L.off_shgrid + (L.has_shg ? sizeof(unsigned long long) * SHGRID_N * SHGRID_N * (size_t)n_lights : 0));
+    L.bytes = al(L.off_shslab + (L.has_shg ? sizeof(unsigned long long) * (SHGRID_SLABS + 2) * (size_t)n_lights : 0)) + 256;
 
     std::vector<unsigned char> blob(L.bytes, 0);
     DevSphere* sph = (DevSphere*)(blob.data() + L.off_sph);
@@ -713,6 +865,12 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
         cull[i] = DevSphereCull{sph[i].cx, sph[i].cy, sph[i].cz, std::nextafter((float)rr, INFINITY)};
     }
     for (int i = n_spheres; i < s_pad; ++i) sph[i] = DevSphere{NAN, NAN, NAN, NAN};
+    DevSpherePair* sphp = (DevSpherePair*)(blob.data() + L.off_sphp);
+    for (int k = 0; k < s_pad / 2; ++k)
+        for (int h = 0; h < 2; ++h) {
+            const DevSphere& e = sph[2 * k + h];
+            sphp[k].cx[h] = e.cx, sphp[k].cy[h] = e.cy, sphp[k].cz[h] = e.cz, sphp[k].r2[h] = e.r2;
+        }
     L.host_sph.assign(sph, sph + n_spheres);
     for (int i = 0; i < n_planes; ++i) {
         const rt_plane& p = planes[i];
@@ -730,6 +888,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
         pl[i] = d;
         mat[n_spheres + i] = dev_material(p.material, ambient);
     }
+    std::vector<Frame3> frames((size_t)n_lights);
     for (int i = 0; i < n_lights; ++i) {
         const rt_light& l = lights[i];
         const H3 p = h3(l.position);
@@ -753,7 +912,13 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
         d.ux = (float)U[0], d.uy = (float)U[1], d.uz = (float)U[2];
         d.vx = (float)V[0], d.vy = (float)V[1], d.vz = (float)V[2];
         li[i] = d;
+        for (int k = 0; k < 3; ++k) frames[(size_t)i].U[k] = U[k], frames[(size_t)i].V[k] = V[k], frames[(size_t)i].A[k] = A[k];
     }
+    if (L.has_shg)
+        for (int j = 0; j < n_lights; ++j)
+            build_shadow_grid(li[j], frames[(size_t)j], sph, cull, n_spheres, ((DevShadowGrid*)(blob.data() + L.off_shg))[j],
+                              (unsigned long long*)(blob.data() + L.off_shgrid) + (size_t)j * SHGRID_N * SHGRID_N,
+                              (unsigned long long*)(blob.data() + L.off_shslab) + (size_t)j * (SHGRID_SLABS + 2));
     if (L.has_shcull) {  // sphere centres in each light's shadow-cull frame (culling only)
         DevShadowCull* sc = (DevShadowCull*)(blob.data() + L.off_shcull);
         for (int j = 0; j < n_lights; ++j)
@@ -780,7 +945,8 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
         if (rc != RT_OK) return rc;
         HIP_TRY(ctx, hipMemcpy(d.d_scene, blob.data(), L.bytes, hipMemcpyHostToDevice));
     }
-    ctx->layout = L;
+    L.host_blob = std::move(blob);
+    ctx->layout = std::move(L);
     ctx->has_scene = true;
     ctx->view_ok = false;
     return RT_OK;

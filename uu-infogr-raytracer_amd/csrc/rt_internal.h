@@ -58,6 +58,14 @@ struct DevLight {
     float vx, vy, vz, pad3;
 };
 
+// Sphere pairs (2k, 2k + 1) of the even-padded DevSphere table, component-interleaved so that a
+// pair's centres and radii^2 load as SGPR pairs: the direct kernel's sphere loops run
+// IntersectsSphere's binary32 products and sums for two spheres per packed instruction
+// (v_pk_mul_f32 / v_pk_add_f32: the same IEEE operations, rounded separately, no contraction).
+struct alignas(32) DevSpherePair {
+    float cx[2], cy[2], cz[2], r2[2];
+};
+
 // Per-sphere culling record: centre and a radius bound r' >= sqrt(r^2) * (1 + 2^-8).
 struct DevSphereCull {
     float cx, cy, cz, rr;
@@ -71,6 +79,32 @@ struct DevShadowCull {
     float cu, cv, ca, rr;
 };
 constexpr long long SHADOW_CULL_MAX_ENTRIES = 1LL << 16;
+
+// Per-light shadow grid (bundle kernel's merged shadow pass, S <= 64 spheres, L <= 4 lights;
+// culling only).  Every shadow ray of light l has direction p_l, so whether sphere j can block a
+// hit point hp depends on hp's coordinates (u, v) across the light's axis and a along it.  The host
+// tabulates, per light, a SHGRID_N x SHGRID_N grid over (u, v) of 64-bit masks -- the spheres whose
+// margin-grown disc reaches the cell -- and SHGRID_SLABS + 2 axial masks -- the spheres whose
+// centre may lie ahead of a slab -- valid for lanes with |hp|_1 <= `bound`; each lane looks up its
+// own cell and slab (rt_kernel.hip shadow_members_grid).  Lanes beyond the bound use the bounding
+// box of every disc with their own margin and the slab masks shifted by it.  Margins and the
+// exactness argument: rt_api.cpp build_shadow_grid.
+// The merged shadow pass (and so the grid) serves scenes with at most 64 spheres and this many lights.
+constexpr int SHADOW_MERGE_L = 4;
+constexpr int SHGRID_N = 64;
+constexpr int SHGRID_SLABS = 32;
+struct DevShadowGrid {
+    float su, ou, sv, ov;  // cell coordinates: floor(fma(u, su, ou)), floor(fma(v, sv, ov))
+    float sa, oa;          // slab coordinate: floor(fma(a, sa, oa)), clamped to [-1, SHGRID_SLABS]
+    float bound;           // lanes with |hp|_1 <= bound use the grid
+    float far_k;           // lanes beyond it: own margin far_k * |hp|_1 (2^-8 + projection error) ...
+    float far_b;           // ... and slab coordinate a - (far_k * |hp|_1 - far_b), far_b = 2^-8 bound
+    float bu0, bu1, bv0, bv1;  // (u, v) box of every sphere's disc grown by 2^-8 |C|_1 (no |hp| term)
+    float pad;
+    unsigned long long always;  // spheres never culled (no valid cull record: NaN/huge/tiny)
+};
+// Device layout: DevShadowGrid[L], then masks [L][SHGRID_N * SHGRID_N] (row iv, column iu), then
+// slab masks [L][SHGRID_SLABS + 2] (entry ia + 1, ia = -1 .. SHGRID_SLABS).
 
 // Work counters: each workgroup adds its totals into slot (block id % COUNTER_SLOTS) so that
 // the atomics of thousands of workgroups do not serialise on one address.  Per slot:
@@ -109,7 +143,11 @@ struct LaunchParams {
     const DevPlane* pl;
     const DevLight* li;
     const DevSphereCull* scull;  // [S]
+    const DevSpherePair* sphp;   // [(S + 1) / 2]
     const DevShadowCull* shcull;  // [L][S] or NULL (no shadow culling)
+    const DevShadowGrid* shg;     // [L] or NULL (no shadow grid: the per-level bound instead)
+    const unsigned long long* shgrid;  // [L][SHGRID_N^2]
+    const unsigned long long* shslab;  // [L][SHGRID_SLABS + 2]
     const float* lxt;  // [W]: ((float)x / W - 0.5f) * pw, TracePixel :963-965
     const float* lyt;  // [H]: ((float)y / H - 0.5f) * ph
     int S, P, L, limit;

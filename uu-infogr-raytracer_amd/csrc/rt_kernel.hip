@@ -137,13 +137,17 @@ __device__ __forceinline__ float root_full(float b, float disc, float a2) {
 // A2OK: 2a is finite and > 0 for every active lane (checked once per segment with a ballot,
 // so the sphere loops carry no per-lane two-way split).
 template <bool A2OK>
+__device__ __forceinline__ float root_sel(float b, float disc, float a2, bool a2_ok) {
+    if constexpr (A2OK) return root_t1(b, disc, a2);
+    else return a2_ok ? root_t1(b, disc, a2) : root_full(b, disc, a2);
+}
+template <bool A2OK>
 __device__ __forceinline__ float sphere_t(f3 o, f3 d, float a2, float a4, bool a2_ok, const DevSphere& s) {
     const f3 oc = sub(o, mk(s.cx, s.cy, s.cz));
     const float b = 2.0f * dot(oc, d);
     const float c = dot(oc, oc) - s.r2;
     const float disc = b * b - a4 * c;
-    if constexpr (A2OK) return root_t1(b, disc, a2);
-    else return a2_ok ? root_t1(b, disc, a2) : root_full(b, disc, a2);
+    return root_sel<A2OK>(b, disc, a2, a2_ok);
 }
 
 // Shadow ray of IntersectShadowLight (origin = hit point, direction = light POSITION,
@@ -156,11 +160,7 @@ __device__ __forceinline__ float sphere_t(f3 o, f3 d, float a2, float a4, bool a
 // paired candidates); in the direct kernel the division-free form measured slower (C2 +4 %, C3
 // +6 %: the shading code around it was scheduled worse), so it keeps the division there.
 template <bool A2OK, bool THRESH = false>
-__device__ __forceinline__ bool shadow_blocked(f3 hp, const DevLight& l, bool a2_ok, const DevSphere& s) {
-    const f3 oc = sub(hp, mk(s.cx, s.cy, s.cz));
-    const float b = 2.0f * dot(oc, mk(l.px, l.py, l.pz));
-    const float c = dot(oc, oc) - s.r2;
-    const float disc = b * b - l.a4 * c;
+__device__ __forceinline__ bool shadow_decide(float b, float disc, const DevLight& l, bool a2_ok) {
     if (A2OK || a2_ok) {
         bool hit = false;
         if (__builtin_amdgcn_ballot_w64(sphere_candidate(b, disc)) != 0) {  // wave-uniform
@@ -177,6 +177,34 @@ __device__ __forceinline__ bool shadow_blocked(f3 hp, const DevLight& l, bool a2
         return nmin(nmax0(t1 - 0.001f), nmax0(t2 - 0.001f)) > 0.0f;
     }
     return false;
+}
+template <bool A2OK, bool THRESH = false>
+__device__ __forceinline__ bool shadow_blocked(f3 hp, const DevLight& l, bool a2_ok, const DevSphere& s) {
+    const f3 oc = sub(hp, mk(s.cx, s.cy, s.cz));
+    const float b = 2.0f * dot(oc, mk(l.px, l.py, l.pz));
+    const float c = dot(oc, oc) - s.r2;
+    const float disc = b * b - l.a4 * c;
+    return shadow_decide<A2OK, THRESH>(b, disc, l, a2_ok);
+}
+
+// IntersectsSphere's b and discriminant for spheres 2k and 2k + 1 (DevSpherePair) and one ray
+// (o, d) with a4 = 4 d.d: the operations of sphere_t / shadow_blocked in the same order, each
+// instruction on both spheres (v_pk_add_f32 / v_pk_mul_f32 with the pair's SGPR operands), so
+// every value is the same binary32 result.
+#ifndef RT_PACKED
+#define RT_PACKED 1
+#endif
+typedef float pf2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ pf2 pk2(float x) { return (pf2)(x); }
+__device__ __forceinline__ pf2 ld2(const float (&a)[2]) { return *(const pf2*)a; }
+struct BD2 {
+    pf2 b, disc;
+};
+__device__ __forceinline__ BD2 sphere_bd_pair(f3 o, f3 d, float a4, const DevSpherePair& s) {
+    const pf2 ox = pk2(o.x) - ld2(s.cx), oy = pk2(o.y) - ld2(s.cy), oz = pk2(o.z) - ld2(s.cz);  // sub(o, c)
+    const pf2 b = pk2(2.0f) * ((ox * pk2(d.x) + oy * pk2(d.y)) + oz * pk2(d.z));            // 2 * dot(oc, d)
+    const pf2 c = ((ox * ox + oy * oy) + oz * oz) - ld2(s.r2);                               // dot(oc, oc) - r^2
+    return BD2{b, b * b - pk2(a4) * c};
 }
 
 // IntersectPlane, RayTracer.cs:590-604: t = (((-o.x*n.x) - o.y*n.y) - o.z*n.z + c.n) / d.n,
@@ -560,11 +588,18 @@ template <bool A2OK, typename T>
 __device__ __forceinline__ bool shadow_scan(const LaunchParams& p, f3 hp, const DevLight& l, T& tl) {
     int blk = 0;
     for_sphere_pairs<T>(p, [&](int i) {
-        const DevSphere s0 = p.sph[i], s1 = p.sph[i + 1];
         tl.shadow_sphere(blk == 0);
-        blk = shadow_blocked<A2OK>(hp, l, false, s0) ? 1 : blk;
-        tl.shadow_sphere((blk == 0) & (i + 1 < p.S));
-        blk = shadow_blocked<A2OK>(hp, l, false, s1) ? 1 : blk;
+        if constexpr (RT_PACKED) {
+            const BD2 q = sphere_bd_pair(hp, mk(l.px, l.py, l.pz), l.a4, p.sphp[i >> 1]);
+            blk = shadow_decide<A2OK>(q.b.x, q.disc.x, l, false) ? 1 : blk;
+            tl.shadow_sphere((blk == 0) & (i + 1 < p.S));
+            blk = shadow_decide<A2OK>(q.b.y, q.disc.y, l, false) ? 1 : blk;
+        } else {
+            const DevSphere s0 = p.sph[i], s1 = p.sph[i + 1];
+            blk = shadow_blocked<A2OK>(hp, l, false, s0) ? 1 : blk;
+            tl.shadow_sphere((blk == 0) & (i + 1 < p.S));
+            blk = shadow_blocked<A2OK>(hp, l, false, s1) ? 1 : blk;
+        }
     });
     return blk != 0;
 }
@@ -689,11 +724,18 @@ __device__ __forceinline__ void nearest_spheres(const LaunchParams& p, f3 o, f3 
     } else {
         // pairs (the device table is padded to an even count with a sphere that never hits)
         for_sphere_pairs<T>(p, [&](int i) {
-            const DevSphere s0 = p.sph[i], s1 = p.sph[i + 1];
             tl.sphere(true);
             tl.sphere(i + 1 < p.S);
-            const float t0 = sphere_t<A2OK>(o, d, a2, a4, a2_ok, s0);
-            const float t1 = sphere_t<A2OK>(o, d, a2, a4, a2_ok, s1);
+            float t0, t1;
+            if constexpr (RT_PACKED) {
+                const BD2 q = sphere_bd_pair(o, d, a4, p.sphp[i >> 1]);
+                t0 = root_sel<A2OK>(q.b.x, q.disc.x, a2, a2_ok);
+                t1 = root_sel<A2OK>(q.b.y, q.disc.y, a2, a2_ok);
+            } else {
+                const DevSphere s0 = p.sph[i], s1 = p.sph[i + 1];
+                t0 = sphere_t<A2OK>(o, d, a2, a4, a2_ok, s0);
+                t1 = sphere_t<A2OK>(o, d, a2, a4, a2_ok, s1);
+            }
             if (PRIMARY) {
                 take_primary(t0, i, best_s, win_s);
                 take_primary(t1, i + 1, best_s, win_s);
@@ -830,8 +872,13 @@ __device__ __forceinline__ unsigned trace_tile_direct(const LaunchParams& p, int
 // STATS: the diagnostic build that also tallies the work actually executed (not timed).
 // TILES: out_fmt OUT_TILES (the fused encoder: its own instantiation, so that the others keep their
 // register budget -- the epilogue alone raises the direct kernel's SGPR peak from 79 to 83).
+// SGPR cap: 80 keeps 8 waves per SIMD (800 / (ceil(sgpr / 16) * 16 + 16), see the bundle kernel);
+// the packed sphere pairs hold their splat operands as SGPR pairs (90 uncapped).
+#ifndef RT_DIRECT_SGPR
+#define RT_DIRECT_SGPR 80
+#endif
 template <int K, bool GPOW, bool STATS, int SMAX, bool TILES>
-__global__ __launch_bounds__(WG_THREADS) void trace_direct_kernel(LaunchParams p) {
+__global__ __launch_bounds__(WG_THREADS, 8) __attribute__((amdgpu_num_sgpr(RT_DIRECT_SGPR))) void trace_direct_kernel(LaunchParams p) {
     constexpr int LDS_LEVELS = StackFor<K>::lds_levels;  // LdsStack slots, else unused
     __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
     __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * WG_THREADS : 1];
@@ -1140,7 +1187,6 @@ __device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d,
 // IntersectShadowLight's :574-578), so every outcome is the same bit.  Returns the lane's blocked
 // bits (bit li).  `want` (bit li): the lane's ray toward light li must be resolved -- a superset of
 // the shading's `need` (shade_bundle), so every needed outcome is computed.
-constexpr int SHADOW_MERGE_L = 4;
 // Candidate sets of the lights as one register: lane i holds bit li when sphere i is a candidate
 // for light li (lights some lane wants only).  Converged call.  (Hoisting the light-independent
 // terms of the cull out of the light loop cut VALU 1.8 % but spilled 12 B/lane: C4 +0.8 %, C5 +0.8 %,
@@ -1155,6 +1201,61 @@ __device__ __forceinline__ unsigned shadow_members(const LaunchParams& p, const 
         }
     return memb;
 }
+// OR of a 32-bit value over the wave (all 64 lanes active): DPP row rotations give each 16-lane row
+// its OR, four readlanes finish it.
+__device__ __forceinline__ unsigned wave_or(unsigned v) {
+    v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x121, 0xf, 0xf, false);  // row_ror:1
+    v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x122, 0xf, 0xf, false);  // row_ror:2
+    v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x124, 0xf, 0xf, false);  // row_ror:4
+    v |= (unsigned)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false);  // row_ror:8
+    return (unsigned)__builtin_amdgcn_readlane((int)v, 0) | (unsigned)__builtin_amdgcn_readlane((int)v, 16) |
+           (unsigned)__builtin_amdgcn_readlane((int)v, 32) | (unsigned)__builtin_amdgcn_readlane((int)v, 48);
+}
+
+// Candidate sets of the lights from the per-light shadow grids (p.shg != nullptr; rt_internal.h
+// DevShadowGrid, host tables and the exactness argument in rt_api.cpp build_shadow_grid): each
+// lane wanting light li looks up the grid cell of its own hit point's (u, v) and the axial slab of
+// its a, ANDs the two masks, and the wave ORs them -- the union of per-lane sets instead of one bound
+// around every lane's hit point, which grows with their spread (deep fold levels, where the hit
+// points of a wave scatter over the scene; tools/shadow_cull_model.py: C4 sphere-light pairs per
+// wave 27.4 -> 7.2).  Culling-only arithmetic (FMA allowed; the margins cover the projections'
+// rounding).  Same result layout as shadow_members.  Converged call.
+__device__ __forceinline__ unsigned shadow_members_grid(const LaunchParams& p, f3 hp, unsigned want) {
+    const int lane = threadIdx.x & 63;
+    const float l1 = __builtin_fabsf(hp.x) + __builtin_fabsf(hp.y) + __builtin_fabsf(hp.z);
+    unsigned memb = 0;
+    for (int li = 0; li < p.L; ++li) {
+        const bool w = (want >> li) & 1u;
+        if (__builtin_amdgcn_ballot_w64(w) == 0) continue;  // wave-uniform
+        const DevShadowGrid& g = p.shg[li];
+        const DevLight& l = p.li[li];
+        const float u = __builtin_fmaf(hp.z, l.uz, __builtin_fmaf(hp.y, l.uy, hp.x * l.ux));
+        const float v = __builtin_fmaf(hp.z, l.vz, __builtin_fmaf(hp.y, l.vy, hp.x * l.vx));
+        const float a = __builtin_fmaf(hp.z, l.az, __builtin_fmaf(hp.y, l.ay, hp.x * l.ax));
+        const bool near = l1 <= g.bound;  // NaN: far
+        // grid cell (near lanes): outside the grid no disc reaches the lane
+        const float xu = __builtin_fmaf(u, g.su, g.ou), xv = __builtin_fmaf(v, g.sv, g.ov);
+        const bool in_grid = xu >= 0.0f && xu < (float)SHGRID_N && xv >= 0.0f && xv < (float)SHGRID_N;
+        const int iu = (int)__builtin_fminf(__builtin_fmaxf(xu, 0.0f), (float)(SHGRID_N - 1));
+        const int iv = (int)__builtin_fminf(__builtin_fmaxf(xv, 0.0f), (float)(SHGRID_N - 1));
+        const unsigned long long cell = p.shgrid[(size_t)li * (SHGRID_N * SHGRID_N) + iv * SHGRID_N + iu];
+        // far lanes: the box of every disc grown by the lane's own margin (NaN: inside)
+        const float mg = g.far_k * l1;
+        const bool in_box = !(u < g.bu0 - mg || u > g.bu1 + mg || v < g.bv0 - mg || v > g.bv1 + mg);
+        // slab of a (far lanes: lowered by their extra margin); NaN and below the range: entry 0 (all)
+        const float af = near ? a : a - (mg - g.far_b);
+        const float xa = __builtin_fminf(__builtin_fmaxf(__builtin_floorf(__builtin_fmaf(af, g.sa, g.oa)), -1.0f),
+                                         (float)SHGRID_SLABS);
+        const unsigned long long slab = p.shslab[(size_t)li * (SHGRID_SLABS + 2) + (int)xa + 1];
+        const bool take = w && (near ? in_grid : in_box);
+        const unsigned long long m = take ? (near ? cell : ~0ull) & slab : 0ull;
+        const unsigned long long cm = ((unsigned long long)wave_or((unsigned)(m >> 32)) << 32) |
+                                      (unsigned long long)wave_or((unsigned)m) | g.always;
+        memb |= ((cm >> lane) & 1ull) ? (1u << li) : 0u;
+    }
+    return memb;
+}
+
 template <typename T>
 __device__ __forceinline__ unsigned shadow_merged(const LaunchParams& p, unsigned memb, f3 hp, unsigned want, bool diff,
                                                   bool act, T& tl) {
@@ -1219,7 +1320,9 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
         for (int li = 0; li < p.L; ++li) tl.shadow(diff);  // (diagnostic tally of the rays resolved)
     if (merged) {
         const unsigned want = diff ? (1u << p.L) - 1u : 0u;
-        blk = shadow_merged(p, shadow_members(p, make_shadow_sphere(hp, diff), want), hp, want, diff, act, tl);
+        const unsigned memb = p.shg ? shadow_members_grid(p, hp, want)  // (wave-uniform choice)
+                                    : shadow_members(p, make_shadow_sphere(hp, diff), want);
+        blk = shadow_merged(p, memb, hp, want, diff, act, tl);
     }
     f3 normal;
     float tile = 1.0f;
