@@ -253,16 +253,16 @@ unsigned long long grid_lookup(const DevShadowGrid& g, const DevLight& l, const 
     const float a = std::fmaf(hp.z, l.az, std::fmaf(hp.y, l.ay, hp.x * l.ax));
     const bool near = l1 <= g.bound;
     const float xu = std::fmaf(u, g.su, g.ou), xv = std::fmaf(v, g.sv, g.ov);
-    const bool in_grid = xu >= 0.0f && xu < (float)SHGRID_N && xv >= 0.0f && xv < (float)SHGRID_N;
-    const int iu = (int)std::fmin(std::fmax(xu, 0.0f), (float)(SHGRID_N - 1));
-    const int iv = (int)std::fmin(std::fmax(xv, 0.0f), (float)(SHGRID_N - 1));
+    const bool in_grid = (xu >= 0.0f) & (xu < (float)SHGRID_N) & (xv >= 0.0f) & (xv < (float)SHGRID_N);
+    const unsigned iu = (unsigned)std::fmin(std::fmax(xu, 0.0f), (float)(SHGRID_N - 1));
+    const unsigned iv = (unsigned)std::fmin(std::fmax(xv, 0.0f), (float)(SHGRID_N - 1));
     const unsigned long long cell = grid[iv * SHGRID_N + iu];
     const float mg = g.far_k * l1;
-    const bool in_box = !(u < g.bu0 - mg || u > g.bu1 + mg || v < g.bv0 - mg || v > g.bv1 + mg);
     const float af = near ? a : a - (mg - g.far_b);
     const float xa = std::fmin(std::fmax(std::floor(std::fmaf(af, g.sa, g.oa)), -1.0f), (float)SHGRID_SLABS);
-    const unsigned long long sl = slab[(int)xa + 1];
-    const bool take = near ? in_grid : in_box;
+    const unsigned long long sl = slab[(unsigned)((int)xa + 1)];
+    const bool out_box = (u < g.bu0 - mg) | (u > g.bu1 + mg) | (v < g.bv0 - mg) | (v > g.bv1 + mg);
+    const bool take = near ? in_grid : !out_box;
     return (take ? (near ? cell : ~0ull) & sl : 0ull) | g.always;
 }
 

@@ -59,3 +59,24 @@ def test_rank_world_mismatch_fails():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"], env=env,
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "WORLD_SIZE=3 but --gpus 2" in r.stderr
+
+
+def test_cpu_baseline_reports_its_spread():
+    """The CPU leg reports the frame-time spread, the CPU time the process was actually given and the
+    cgroup's throttling over each sample beside the median (the driver's CPU figure
+    varied 28 % between boxes with nothing in the line to explain it)."""
+    from raytracer_hip import scenes
+    sc = scenes.config("C1").resized(64, 48)
+    out = bench.cpu_baseline([(sc, None, 0.6), (scenes.reference(32, 32), None, 0.4)], 0.3)
+    for e in (out, out["others"]["ref"]):
+        p10, p50, p90 = e["frame_ms_p10_p50_p90"]
+        assert 0 < p10 <= p50 <= p90 and e["frames"] >= 3
+        assert e["cpus_scheduled"] >= 0
+        t = e["cgroup_throttled"]
+        assert t is None or (t["periods"] >= 0 and t["nr_throttled"] >= 0 and t["throttled_ms"] >= 0)
+    assert out["cores"] >= 1 and "frame_ms_p10_p50_p90" in out["sample"]
+
+
+def test_percentiles_nearest_rank():
+    assert bench.percentiles([5, 1, 2, 3, 4]) == [1, 3, 5]
+    assert bench.percentiles([7]) == [7, 7, 7]

@@ -194,6 +194,9 @@ __device__ __forceinline__ bool shadow_blocked(f3 hp, const DevLight& l, bool a2
 #ifndef RT_PACKED
 #define RT_PACKED 1
 #endif
+#ifndef RT_DIRECT_THRESH
+#define RT_DIRECT_THRESH false
+#endif
 typedef float pf2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ pf2 pk2(float x) { return (pf2)(x); }
 __device__ __forceinline__ pf2 ld2(const float (&a)[2]) { return *(const pf2*)a; }
@@ -591,9 +594,9 @@ __device__ __forceinline__ bool shadow_scan(const LaunchParams& p, f3 hp, const 
         tl.shadow_sphere(blk == 0);
         if constexpr (RT_PACKED) {
             const BD2 q = sphere_bd_pair(hp, mk(l.px, l.py, l.pz), l.a4, p.sphp[i >> 1]);
-            blk = shadow_decide<A2OK>(q.b.x, q.disc.x, l, false) ? 1 : blk;
+            blk = shadow_decide<A2OK, RT_DIRECT_THRESH>(q.b.x, q.disc.x, l, false) ? 1 : blk;
             tl.shadow_sphere((blk == 0) & (i + 1 < p.S));
-            blk = shadow_decide<A2OK>(q.b.y, q.disc.y, l, false) ? 1 : blk;
+            blk = shadow_decide<A2OK, RT_DIRECT_THRESH>(q.b.y, q.disc.y, l, false) ? 1 : blk;
         } else {
             const DevSphere s0 = p.sph[i], s1 = p.sph[i + 1];
             blk = shadow_blocked<A2OK>(hp, l, false, s0) ? 1 : blk;
@@ -1233,21 +1236,22 @@ __device__ __forceinline__ unsigned shadow_members_grid(const LaunchParams& p, f
         const float v = __builtin_fmaf(hp.z, l.vz, __builtin_fmaf(hp.y, l.vy, hp.x * l.vx));
         const float a = __builtin_fmaf(hp.z, l.az, __builtin_fmaf(hp.y, l.ay, hp.x * l.ax));
         const bool near = l1 <= g.bound;  // NaN: far
-        // grid cell (near lanes): outside the grid no disc reaches the lane
+        // grid cell (near lanes): outside the grid no disc reaches the lane.  Branch-free (bitwise
+        // ands / ors): both table loads are issued unconditionally, at clamped in-range indices
         const float xu = __builtin_fmaf(u, g.su, g.ou), xv = __builtin_fmaf(v, g.sv, g.ov);
-        const bool in_grid = xu >= 0.0f && xu < (float)SHGRID_N && xv >= 0.0f && xv < (float)SHGRID_N;
-        const int iu = (int)__builtin_fminf(__builtin_fmaxf(xu, 0.0f), (float)(SHGRID_N - 1));
-        const int iv = (int)__builtin_fminf(__builtin_fmaxf(xv, 0.0f), (float)(SHGRID_N - 1));
-        const unsigned long long cell = p.shgrid[(size_t)li * (SHGRID_N * SHGRID_N) + iv * SHGRID_N + iu];
-        // far lanes: the box of every disc grown by the lane's own margin (NaN: inside)
-        const float mg = g.far_k * l1;
-        const bool in_box = !(u < g.bu0 - mg || u > g.bu1 + mg || v < g.bv0 - mg || v > g.bv1 + mg);
+        const bool in_grid = (xu >= 0.0f) & (xu < (float)SHGRID_N) & (xv >= 0.0f) & (xv < (float)SHGRID_N);
+        const unsigned iu = (unsigned)__builtin_fminf(__builtin_fmaxf(xu, 0.0f), (float)(SHGRID_N - 1));
+        const unsigned iv = (unsigned)__builtin_fminf(__builtin_fmaxf(xv, 0.0f), (float)(SHGRID_N - 1));
+        const unsigned long long cell = p.shgrid[(unsigned)li * (SHGRID_N * SHGRID_N) + iv * SHGRID_N + iu];
         // slab of a (far lanes: lowered by their extra margin); NaN and below the range: entry 0 (all)
+        const float mg = g.far_k * l1;
         const float af = near ? a : a - (mg - g.far_b);
         const float xa = __builtin_fminf(__builtin_fmaxf(__builtin_floorf(__builtin_fmaf(af, g.sa, g.oa)), -1.0f),
                                          (float)SHGRID_SLABS);
-        const unsigned long long slab = p.shslab[(size_t)li * (SHGRID_SLABS + 2) + (int)xa + 1];
-        const bool take = w && (near ? in_grid : in_box);
+        const unsigned long long slab = p.shslab[(unsigned)li * (SHGRID_SLABS + 2) + (unsigned)((int)xa + 1)];
+        // far lanes: the box of every disc grown by the lane's own margin (NaN: inside)
+        const bool out_box = (u < g.bu0 - mg) | (u > g.bu1 + mg) | (v < g.bv0 - mg) | (v > g.bv1 + mg);
+        const bool take = w & (near ? in_grid : !out_box);
         const unsigned long long m = take ? (near ? cell : ~0ull) & slab : 0ull;
         const unsigned long long cm = ((unsigned long long)wave_or((unsigned)(m >> 32)) << 32) |
                                       (unsigned long long)wave_or((unsigned)m) | g.always;
