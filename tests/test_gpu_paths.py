@@ -194,8 +194,9 @@ def test_driver_shape_forced_repeat_counts_one_attempt():
     for margin in ("1.25", "0.5"):
         env = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()))
         env.pop("WORLD_SIZE", None)
-        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--dist-path", "--config", "C2", "--steps", "20",
-               "--warmup", "5", "--no-cpu-baseline", "--also-dist", "", "--spec-margin", margin]
+        # (--rank0-codec: rank 0 ships its own bands through the codec, so the world-1 wire is not empty)
+        cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--dist-path", "--rank0-codec", "--config", "C2",
+               "--steps", "20", "--warmup", "5", "--no-cpu-baseline", "--also-dist", "", "--spec-margin", margin]
         r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=110)
         assert r.returncode == 0, r.stderr[-2000:]
         lines.append(json.loads(r.stdout.strip().splitlines()[-1]))

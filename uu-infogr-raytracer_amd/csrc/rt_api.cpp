@@ -156,7 +156,7 @@ struct Device {
 struct SceneLayout {
     int S = 0, P = 0, L = 0, limit = 0;
     size_t off_sph = 0, off_mat = 0, off_pl = 0, off_li = 0, off_cull = 0, off_shcull = 0, bytes = 0;
-    size_t off_shg = 0, off_shgrid = 0, off_shslab = 0, off_sphp = 0;
+    size_t off_shg = 0, off_shgrid = 0, off_shslab = 0;
     bool has_shcull = false;
     bool has_shg = false;  // per-light shadow grids (DevShadowGrid) for the merged shadow pass
     std::vector<unsigned char> host_blob;  // the uploaded scene image (host tests read the tables)
@@ -443,7 +443,6 @@ void scene_params(const rt_ctx* ctx, const Device& d, LaunchParams& lp) {
     lp.pl = (const DevPlane*)(base + L.off_pl);
     lp.li = (const DevLight*)(base + L.off_li);
     lp.scull = (const DevSphereCull*)(base + L.off_cull);
-    lp.sphp = (const DevSpherePair*)(base + L.off_sphp);
     lp.shcull = L.has_shcull ? (const DevShadowCull*)(base + L.off_shcull) : nullptr;
     lp.shg = L.has_shg ? (const DevShadowGrid*)(base + L.off_shg) : nullptr;
     lp.shgrid = L.has_shg ? (const unsigned long long*)(base + L.off_shgrid) : nullptr;
@@ -837,8 +836,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
     L.off_pl = al(L.off_mat + sizeof(DevMaterial) * (size_t)(n_spheres + n_planes));
     L.off_li = al(L.off_pl + sizeof(DevPlane) * (size_t)n_planes);
     L.off_cull = al(L.off_li + sizeof(DevLight) * (size_t)n_lights);
-    L.off_sphp = al(L.off_cull + sizeof(DevSphereCull) * (size_t)n_spheres);
-    L.off_shcull = al(L.off_sphp + sizeof(DevSpherePair) * (size_t)(s_pad / 2));
+    L.off_shcull = al(L.off_cull + sizeof(DevSphereCull) * (size_t)n_spheres);
     L.has_shcull = (long long)n_lights * (long long)n_spheres <= SHADOW_CULL_MAX_ENTRIES;
     // shadow grids: the bundle kernel's merged pass only (CULL_MIN_SPHERES <= S <= 64, 1 <= L <=
     // SHADOW_MERGE_L); RT_SHADOW_GRID=0 keeps the per-level bound (A/B and fallback tests)
@@ -865,12 +863,6 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
         cull[i] = DevSphereCull{sph[i].cx, sph[i].cy, sph[i].cz, std::nextafter((float)rr, INFINITY)};
     }
     for (int i = n_spheres; i < s_pad; ++i) sph[i] = DevSphere{NAN, NAN, NAN, NAN};
-    DevSpherePair* sphp = (DevSpherePair*)(blob.data() + L.off_sphp);
-    for (int k = 0; k < s_pad / 2; ++k)
-        for (int h = 0; h < 2; ++h) {
-            const DevSphere& e = sph[2 * k + h];
-            sphp[k].cx[h] = e.cx, sphp[k].cy[h] = e.cy, sphp[k].cz[h] = e.cz, sphp[k].r2[h] = e.r2;
-        }
     L.host_sph.assign(sph, sph + n_spheres);
     for (int i = 0; i < n_planes; ++i) {
         const rt_plane& p = planes[i];

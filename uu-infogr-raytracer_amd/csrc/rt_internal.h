@@ -58,14 +58,6 @@ struct DevLight {
     float vx, vy, vz, pad3;
 };
 
-// Sphere pairs (2k, 2k + 1) of the even-padded DevSphere table, component-interleaved so that a
-// pair's centres and radii^2 load as SGPR pairs: the direct kernel's sphere loops run
-// IntersectsSphere's binary32 products and sums for two spheres per packed instruction
-// (v_pk_mul_f32 / v_pk_add_f32: the same IEEE operations, rounded separately, no contraction).
-struct alignas(32) DevSpherePair {
-    float cx[2], cy[2], cz[2], r2[2];
-};
-
 // Per-sphere culling record: centre and a radius bound r' >= sqrt(r^2) * (1 + 2^-8).
 struct DevSphereCull {
     float cx, cy, cz, rr;
@@ -143,7 +135,6 @@ struct LaunchParams {
     const DevPlane* pl;
     const DevLight* li;
     const DevSphereCull* scull;  // [S]
-    const DevSpherePair* sphp;   // [(S + 1) / 2]
     const DevShadowCull* shcull;  // [L][S] or NULL (no shadow culling)
     const DevShadowGrid* shg;     // [L] or NULL (no shadow grid: the per-level bound instead)
     const unsigned long long* shgrid;  // [L][SHGRID_N^2]

@@ -187,28 +187,6 @@ __device__ __forceinline__ bool shadow_blocked(f3 hp, const DevLight& l, bool a2
     return shadow_decide<A2OK, THRESH>(b, disc, l, a2_ok);
 }
 
-// IntersectsSphere's b and discriminant for spheres 2k and 2k + 1 (DevSpherePair) and one ray
-// (o, d) with a4 = 4 d.d: the operations of sphere_t / shadow_blocked in the same order, each
-// instruction on both spheres (v_pk_add_f32 / v_pk_mul_f32 with the pair's SGPR operands), so
-// every value is the same binary32 result.
-#ifndef RT_PACKED
-#define RT_PACKED 1
-#endif
-#ifndef RT_DIRECT_THRESH
-#define RT_DIRECT_THRESH false
-#endif
-typedef float pf2 __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ pf2 pk2(float x) { return (pf2)(x); }
-__device__ __forceinline__ pf2 ld2(const float (&a)[2]) { return *(const pf2*)a; }
-struct BD2 {
-    pf2 b, disc;
-};
-__device__ __forceinline__ BD2 sphere_bd_pair(f3 o, f3 d, float a4, const DevSpherePair& s) {
-    const pf2 ox = pk2(o.x) - ld2(s.cx), oy = pk2(o.y) - ld2(s.cy), oz = pk2(o.z) - ld2(s.cz);  // sub(o, c)
-    const pf2 b = pk2(2.0f) * ((ox * pk2(d.x) + oy * pk2(d.y)) + oz * pk2(d.z));            // 2 * dot(oc, d)
-    const pf2 c = ((ox * ox + oy * oy) + oz * oz) - ld2(s.r2);                               // dot(oc, oc) - r^2
-    return BD2{b, b * b - pk2(a4) * c};
-}
 
 // IntersectPlane, RayTracer.cs:590-604: t = (((-o.x*n.x) - o.y*n.y) - o.z*n.z + c.n) / d.n,
 // hit iff t > 0 -- the quotient itself.  (+inf, from a zero denominator, is a "hit" that no
@@ -369,28 +347,28 @@ struct LdsStack {
     int n = 0;
     __device__ __forceinline__ LdsStack(float2* l, float* dd) : lv(l), dv(dd) {}
     __device__ __forceinline__ void origin(f3 d) {
-        dv[threadIdx.x] = d.x;
-        dv[WG_THREADS + threadIdx.x] = d.y;
-        dv[2 * WG_THREADS + threadIdx.x] = d.z;
+        dv[(threadIdx.x & 63)] = d.x;
+        dv[WG_THREADS + (threadIdx.x & 63)] = d.y;
+        dv[2 * WG_THREADS + (threadIdx.x & 63)] = d.z;
     }
     __device__ __forceinline__ void push(float4 x, float4 y) {
-        lv[n * WG_THREADS + threadIdx.x] = make_float2(x.w, y.w);
+        lv[n * WG_THREADS + (threadIdx.x & 63)] = make_float2(x.w, y.w);
         ++n;
     }
     __device__ __forceinline__ void pop(const LaunchParams& p, float4& x, float4& y) {
         --n;
         f3 o = mk(p.cam[0], p.cam[1], p.cam[2]);
-        f3 d = mk(dv[threadIdx.x], dv[WG_THREADS + threadIdx.x], dv[2 * WG_THREADS + threadIdx.x]);
+        f3 d = mk(dv[(threadIdx.x & 63)], dv[WG_THREADS + (threadIdx.x & 63)], dv[2 * WG_THREADS + (threadIdx.x & 63)]);
 #pragma unroll 1
         for (int j = 0; j < K - 1; ++j) {
             const bool go = j < n;
             if (__builtin_amdgcn_ballot_w64(go) == 0) break;
             if (go) {
-                const float2 tc = lv[j * WG_THREADS + threadIdx.x];
+                const float2 tc = lv[j * WG_THREADS + (threadIdx.x & 63)];
                 o = reflect_at(p, o, d, tc.x, __float_as_int(tc.y));
             }
         }
-        const float2 tk = lv[n * WG_THREADS + threadIdx.x];
+        const float2 tk = lv[n * WG_THREADS + (threadIdx.x & 63)];
         const f3 hp = add(o, scale(d, tk.x));
         x = make_float4(hp.x, hp.y, hp.z, tk.x);
         y = make_float4(d.x, d.y, d.z, tk.y);
@@ -592,17 +570,10 @@ __device__ __forceinline__ bool shadow_scan(const LaunchParams& p, f3 hp, const 
     int blk = 0;
     for_sphere_pairs<T>(p, [&](int i) {
         tl.shadow_sphere(blk == 0);
-        if constexpr (RT_PACKED) {
-            const BD2 q = sphere_bd_pair(hp, mk(l.px, l.py, l.pz), l.a4, p.sphp[i >> 1]);
-            blk = shadow_decide<A2OK, RT_DIRECT_THRESH>(q.b.x, q.disc.x, l, false) ? 1 : blk;
-            tl.shadow_sphere((blk == 0) & (i + 1 < p.S));
-            blk = shadow_decide<A2OK, RT_DIRECT_THRESH>(q.b.y, q.disc.y, l, false) ? 1 : blk;
-        } else {
-            const DevSphere s0 = p.sph[i], s1 = p.sph[i + 1];
-            blk = shadow_blocked<A2OK>(hp, l, false, s0) ? 1 : blk;
-            tl.shadow_sphere((blk == 0) & (i + 1 < p.S));
-            blk = shadow_blocked<A2OK>(hp, l, false, s1) ? 1 : blk;
-        }
+        const DevSphere s0 = p.sph[i], s1 = p.sph[i + 1];
+        blk = shadow_blocked<A2OK>(hp, l, false, s0) ? 1 : blk;
+        tl.shadow_sphere((blk == 0) & (i + 1 < p.S));
+        blk = shadow_blocked<A2OK>(hp, l, false, s1) ? 1 : blk;
     });
     return blk != 0;
 }
@@ -729,16 +700,9 @@ __device__ __forceinline__ void nearest_spheres(const LaunchParams& p, f3 o, f3 
         for_sphere_pairs<T>(p, [&](int i) {
             tl.sphere(true);
             tl.sphere(i + 1 < p.S);
-            float t0, t1;
-            if constexpr (RT_PACKED) {
-                const BD2 q = sphere_bd_pair(o, d, a4, p.sphp[i >> 1]);
-                t0 = root_sel<A2OK>(q.b.x, q.disc.x, a2, a2_ok);
-                t1 = root_sel<A2OK>(q.b.y, q.disc.y, a2, a2_ok);
-            } else {
-                const DevSphere s0 = p.sph[i], s1 = p.sph[i + 1];
-                t0 = sphere_t<A2OK>(o, d, a2, a4, a2_ok, s0);
-                t1 = sphere_t<A2OK>(o, d, a2, a4, a2_ok, s1);
-            }
+            const DevSphere s0 = p.sph[i], s1 = p.sph[i + 1];
+            const float t0 = sphere_t<A2OK>(o, d, a2, a4, a2_ok, s0);
+            const float t1 = sphere_t<A2OK>(o, d, a2, a4, a2_ok, s1);
             if (PRIMARY) {
                 take_primary(t0, i, best_s, win_s);
                 take_primary(t1, i + 1, best_s, win_s);
@@ -875,22 +839,24 @@ __device__ __forceinline__ unsigned trace_tile_direct(const LaunchParams& p, int
 // STATS: the diagnostic build that also tallies the work actually executed (not timed).
 // TILES: out_fmt OUT_TILES (the fused encoder: its own instantiation, so that the others keep their
 // register budget -- the epilogue alone raises the direct kernel's SGPR peak from 79 to 83).
-// SGPR cap: 80 keeps 8 waves per SIMD (800 / (ceil(sgpr / 16) * 16 + 16), see the bundle kernel);
-// the packed sphere pairs hold their splat operands as SGPR pairs (90 uncapped).
-#ifndef RT_DIRECT_SGPR
-#define RT_DIRECT_SGPR 80
-#endif
-template <int K, bool GPOW, bool STATS, int SMAX, bool TILES>
-__global__ __launch_bounds__(WG_THREADS, 8) __attribute__((amdgpu_num_sgpr(RT_DIRECT_SGPR))) void trace_direct_kernel(LaunchParams p) {
+// WPG: waves (8x8 tiles of a tile row) per workgroup -- 1 for batch launches; RT_SINGLE_WPG for
+// single-frame launches without a copy slice (fewer, larger workgroups: the dispatcher launches
+// one-wave groups no faster than ~6.9 us per 1080p frame, a floor a lone frame's launch pays in
+// full, tools/launch_probe.hip).  Each wave has its own LDS stack slice.
+template <int K, bool GPOW, bool STATS, int SMAX, bool TILES, int WPG = 1>
+__global__ __launch_bounds__(WG_THREADS * WPG) void trace_direct_kernel(LaunchParams p) {
     constexpr int LDS_LEVELS = StackFor<K>::lds_levels;  // LdsStack slots, else unused
-    __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
-    __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * WG_THREADS : 1];
-    if (blockIdx.z < (unsigned)p.copy_z) {  // wave-uniform: the fused hand-off's copy slice
+    __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS * WPG : 1];
+    __shared__ float stk_dv[LDS_LEVELS > 0 ? 3 * WG_THREADS * WPG : 1];
+    if (WPG == 1 && blockIdx.z < (unsigned)p.copy_z) {  // wave-uniform: the fused hand-off's copy slice
         copy_slice(p);
         return;
     }
     Tally<STATS, SMAX> tl;
-    const unsigned cnt = trace_tile_direct<K, GPOW, TILES>(p, blockIdx.x, stk_lv, stk_dv, tl);
+    const int wave = WPG > 1 ? (int)(threadIdx.x >> 6) : 0;
+    float2* lv = stk_lv + (LDS_LEVELS > 0 ? wave * LDS_LEVELS * WG_THREADS : 0);
+    float* dv = stk_dv + (LDS_LEVELS > 0 ? wave * 3 * WG_THREADS : 0);
+    const unsigned cnt = trace_tile_direct<K, GPOW, TILES>(p, (int)blockIdx.x * WPG + wave, lv, dv, tl);
     add_counters<STATS>(p, threadIdx.x & 63, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
 }
 
@@ -1215,6 +1181,9 @@ __device__ __forceinline__ unsigned wave_or(unsigned v) {
            (unsigned)__builtin_amdgcn_readlane((int)v, 32) | (unsigned)__builtin_amdgcn_readlane((int)v, 48);
 }
 
+#ifndef RT_GRID_FROM_LEVEL
+#define RT_GRID_FROM_LEVEL 1
+#endif
 // Candidate sets of the lights from the per-light shadow grids (p.shg != nullptr; rt_internal.h
 // DevShadowGrid, host tables and the exactness argument in rt_api.cpp build_shadow_grid): each
 // lane wanting light li looks up the grid cell of its own hit point's (u, v) and the axial slab of
@@ -1306,9 +1275,9 @@ __device__ __forceinline__ unsigned shadow_merged(const LaunchParams& p, unsigne
 // the deeper segment `sec`), then each light in order, then ambient.  Inactive lanes
 // return `sec` unchanged.  Shadow rays (IntersectShadowLight :573-582) of the lanes that
 // need them form one bundle per light (common direction = the light position).
-template <bool GPOW, typename T>
+template <bool GPOW, bool MERGED, typename T>
 __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool is_sphere, int prim, f3 hp, f3 d, float t,
-                                           f3 sec, unsigned* n_shadow, T& tl) {
+                                           f3 sec, unsigned* n_shadow, T& tl, int level) {
     // idle lanes (act false) carry a copy of an active lane's record: same branches, result dropped
     const DevMaterial& m = p.mat[is_sphere ? prim : p.S + prim];
     const uint32_t flags = m.flags;
@@ -1318,14 +1287,19 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
     // is resolved (a superset of the shading's `need`); a cheap back-facing filter that skipped
     // some of them measured slower (C4 420 vs 401 us: its arithmetic on every lane of every level
     // cost more than the tests it saved, profiles/ab/r03_shadow_merged.txt).
-    const bool merged = p.S <= 64 && p.L >= 1 && p.L <= SHADOW_MERGE_L && __builtin_amdgcn_ballot_w64(diff) != 0;
+    // MERGED (an instantiation of its own, so that neither path's code and registers burden the
+    // other: S <= 64, 1 <= L <= SHADOW_MERGE_L, chosen on the host)
+    const bool merged = MERGED && __builtin_amdgcn_ballot_w64(diff) != 0;
     unsigned blk = 0u;
     if (merged)
         for (int li = 0; li < p.L; ++li) tl.shadow(diff);  // (diagnostic tally of the rays resolved)
     if (merged) {
         const unsigned want = diff ? (1u << p.L) - 1u : 0u;
-        const unsigned memb = p.shg ? shadow_members_grid(p, hp, want)  // (wave-uniform choice)
-                                    : shadow_members(p, make_shadow_sphere(hp, diff), want);
+        // per-lane grid lookups below the first fold level, where a wave's hit points scatter; at
+        // level 0 (the tile's primary hits, coherent) one bound around them culls tighter than the
+        // grid's cells (wave-uniform choice)
+        const unsigned memb = (p.shg && level >= RT_GRID_FROM_LEVEL) ? shadow_members_grid(p, hp, want)
+                                                                      : shadow_members(p, make_shadow_sphere(hp, diff), want);
         blk = shadow_merged(p, memb, hp, want, diff, act, tl);
     }
     f3 normal;
@@ -1349,7 +1323,7 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
         const float att = is_sphere ? cr_rcp(t) * t : (float)(1.0 / ((double)t * (double)t));
         const f3 kd = mk(m.kd[0], m.kd[1], m.kd[2]);
         ShadowSphere SS{};
-        if (!merged) SS = make_shadow_sphere(hp, diff);  // one bound for every light's shadow rays
+        if (!MERGED) SS = make_shadow_sphere(hp, diff);  // one bound for every light's shadow rays
         unsigned long long umask = 0;  // (diagnostic builds: the union of the lights' candidates)
         for (int li = 0; li < p.L; ++li) {
             const DevLight& l = p.li[li];
@@ -1367,7 +1341,8 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
             ph = add(ph, spec);
             const bool need = diff && shadow_matters(ph, l.intensity, att);
             bool blocked = merged ? ((blk >> li) & 1u) != 0 : !need;
-            if (!merged && __builtin_amdgcn_ballot_w64(need) != 0) {  // some lane's pixel depends on this test
+            if (!MERGED && __builtin_amdgcn_ballot_w64(need) != 0) {  // some lane's pixel depends on this test
+                // (MERGED without a diffuse lane: no lane needs a test)
                 tl.shadow(need);
                 const f3 hs = need ? hp : SS.O;  // idle lanes mirror a shading lane (results ignored)
                 for (int base = 0; base < p.S; base += 64) {
@@ -1415,7 +1390,7 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
 // Backward fold (converged call, all 64 lanes): level by level from the deepest, every recorded
 // hit is shaded; a mirror hit consumes the colour of the segment after it (levels 0..limit push
 // at most one record each, so K = limit + 1 records suffice).  Returns the lane's colour.
-template <bool GPOW, typename STK, typename T>
+template <bool GPOW, bool MERGED, typename STK, typename T>
 __device__ __forceinline__ f3 fold_converged(const LaunchParams& p, STK& stk, f3 leaf, unsigned* cnt, T& tl) {
     f3 col = leaf;
     const int depth = stk.n;
@@ -1439,15 +1414,15 @@ __device__ __forceinline__ f3 fold_converged(const LaunchParams& p, STK& stk, f3
         const int code = __float_as_int(rb.w);
         const bool is_s = code >= 0;
         tl.set_level(level);
-        col = shade_bundle<GPOW>(p, act, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z), ra.w,
-                                 col, cnt, tl);
+        col = shade_bundle<GPOW, MERGED>(p, act, is_s, is_s ? code : ~code, mk(ra.x, ra.y, ra.z), mk(rb.x, rb.y, rb.z),
+                                         ra.w, col, cnt, tl, level);
     }
     return col;
 }
 
 // BUNDLE kernel (scenes with >= CULL_MIN_SPHERES spheres): converged control flow so that
 // every segment and every light can form a wave bundle and cull the sphere list.
-template <int K, bool GPOW, bool TILES, typename T>
+template <int K, bool GPOW, bool TILES, bool MERGED, typename T>
 __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int tile_x, float2* stk_lv, float* stk_dv,
                                                       T& tl) {
     const int lane = threadIdx.x & 63;
@@ -1517,7 +1492,7 @@ __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int
         }
     }
 
-    const f3 col = fold_converged<GPOW>(p, stk, leaf, &cnt, tl);
+    const f3 col = fold_converged<GPOW, MERGED>(p, stk, leaf, &cnt, tl);
     const uint32_t px32 = (shift_channel(col.x) << 16) | (shift_channel(col.y) << 8) | shift_channel(col.z);
     if constexpr (TILES) encode_tile_fused(p, px32, valid);
     else {
@@ -1537,7 +1512,7 @@ __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int
 // spilled to VGPR lanes) and 64 VGPRs (8 waves): C4 -2.6 %, C5 -7.5 %.  Not with GPOW (the f64
 // Math.Pow path would spill ~150 B/lane to scratch).  The direct kernel needs no cap (79 SGPRs, 48
 // VGPRs).
-template <int K, bool GPOW, bool STATS, bool TILES>
+template <int K, bool GPOW, bool STATS, bool TILES, bool MERGED>
 __device__ __forceinline__ void bundle_kernel_body(const LaunchParams& p) {
     constexpr int LDS_LEVELS = StackFor<K>::lds_levels;  // LdsStack slots, else unused
     __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
@@ -1548,17 +1523,17 @@ __device__ __forceinline__ void bundle_kernel_body(const LaunchParams& p) {
     }
     Tally<STATS> tl;
     tl.init(p);
-    const unsigned cnt = trace_tile_bundle<K, GPOW, TILES>(p, blockIdx.x, stk_lv, stk_dv, tl);
+    const unsigned cnt = trace_tile_bundle<K, GPOW, TILES, MERGED>(p, blockIdx.x, stk_lv, stk_dv, tl);
     add_counters<STATS>(p, threadIdx.x & 63, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
 }
-template <int K, bool STATS, bool TILES>
+template <int K, bool STATS, bool TILES, bool MERGED>
 __global__ __launch_bounds__(WG_THREADS, 8) __attribute__((amdgpu_num_sgpr(80))) void trace_bundle_kernel(
     LaunchParams p) {
-    bundle_kernel_body<K, false, STATS, TILES>(p);
+    bundle_kernel_body<K, false, STATS, TILES, MERGED>(p);
 }
-template <int K, bool STATS, bool TILES>
+template <int K, bool STATS, bool TILES, bool MERGED>
 __global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel_gpow(LaunchParams p) {
-    bundle_kernel_body<K, true, STATS, TILES>(p);
+    bundle_kernel_body<K, true, STATS, TILES, MERGED>(p);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1672,18 +1647,24 @@ static void launch_by_depth(const LaunchParams& p, dim3 grid, dim3 block, hipStr
     else if (need <= 8) hipLaunchKernelGGL(KERNEL<8>::fn, grid, block, 0, s, p);
     else hipLaunchKernelGGL(KERNEL<64>::fn, grid, block, 0, s, p);
 }
-template <bool GPOW, bool STATS, int SMAX, bool TILES>
+template <bool GPOW, bool STATS, int SMAX, bool TILES, int WPG = 1>
 struct DirectK {
     template <int K>
     struct at {
-        static constexpr auto fn = trace_direct_kernel<K, GPOW, STATS, SMAX, TILES>;
+        static constexpr auto fn = trace_direct_kernel<K, GPOW, STATS, SMAX, TILES, WPG>;
     };
 };
-template <bool GPOW, bool STATS, bool TILES>
+#ifndef RT_SINGLE_WPG
+#define RT_SINGLE_WPG 1
+#endif
+#ifndef RT_WPG_ALL
+#define RT_WPG_ALL 0
+#endif
+template <bool GPOW, bool STATS, bool TILES, bool MERGED>
 struct BundleK {
     template <int K>
     struct at {
-        static constexpr auto fn = GPOW ? trace_bundle_kernel_gpow<K, STATS, TILES> : trace_bundle_kernel<K, STATS, TILES>;
+        static constexpr auto fn = GPOW ? trace_bundle_kernel_gpow<K, STATS, TILES, MERGED> : trace_bundle_kernel<K, STATS, TILES, MERGED>;
     };
 };
 
@@ -1693,8 +1674,20 @@ constexpr int DIRECT_SMAX = 8;
 
 template <bool GPOW, bool STATS, bool TILES = false>
 static void launch_variant(const LaunchParams& p, bool bundle, dim3 grid, dim3 block, hipStream_t s) {
-    if (bundle) launch_by_depth<BundleK<GPOW, STATS, TILES>::template at>(p, grid, block, s);
-    else if (p.S <= DIRECT_SMAX)
+    if (bundle) {
+        // the merged shadow pass's instantiation for S <= 64 spheres and 1..SHADOW_MERGE_L lights
+        if (p.S <= 64 && p.L >= 1 && p.L <= SHADOW_MERGE_L)
+            launch_by_depth<BundleK<GPOW, STATS, TILES, true>::template at>(p, grid, block, s);
+        else
+            launch_by_depth<BundleK<GPOW, STATS, TILES, false>::template at>(p, grid, block, s);
+    }
+    else if (RT_SINGLE_WPG > 1 && !STATS && !TILES && (RT_WPG_ALL || p.n_frames <= 1) && p.copy_z == 0) {
+        // a lone frame: RT_SINGLE_WPG tiles of a tile row per workgroup
+        const dim3 g((grid.x + RT_SINGLE_WPG - 1) / RT_SINGLE_WPG, grid.y, grid.z), b(WG_THREADS * RT_SINGLE_WPG);
+        if (p.S <= DIRECT_SMAX)
+            launch_by_depth<DirectK<GPOW, false, DIRECT_SMAX, false, RT_SINGLE_WPG>::template at>(p, g, b, s);
+        else launch_by_depth<DirectK<GPOW, false, 0, false, RT_SINGLE_WPG>::template at>(p, g, b, s);
+    } else if (p.S <= DIRECT_SMAX)
         launch_by_depth<DirectK<GPOW, STATS, DIRECT_SMAX, TILES>::template at>(p, grid, block, s);
     else launch_by_depth<DirectK<GPOW, STATS, 0, TILES>::template at>(p, grid, block, s);
 }

@@ -298,6 +298,10 @@ class TileBandGather:
         self.first_rank = 0 if (rank0_codec or self.compositor) else 1
         self.direct = self.root and not rank0_codec and not self.compositor  # rank 0 renders into its frames
         self.idle = self.root and self.compositor  # rank 0 only assembles
+        # a world of one rank that renders straight into its frames has nothing to exchange: no size
+        # reduce, gather or decode is issued (the one-GPU rehearsal of the default path then measures
+        # the trace and the pipeline's bookkeeping alone)
+        self.solo = self.direct and self.pworld == 1
         # fused: this rank traces its bands straight into the wire of the batch (rt_render_bands_tiles;
         # `wire_target`), and stage A's encode(None, ...) only finishes that wire (rt_finish_wire)
         self.fused = bool(fused) and not (self.direct or self.idle)
@@ -465,6 +469,11 @@ class TileBandGather:
     def _stage_a(self, main, n_frames):
         import torch.distributed as dist
         b = self.batch
+        if self.solo:  # the frames are final as traced (stream order)
+            self.batch += 1
+            if self.root:
+                self.decoded += 1
+            return
         i = b % 3
         while self.stage_b and self.stage_b[0][0] <= b - 3:  # (no-ops in steady state)
             self._stage_b()
