@@ -190,6 +190,32 @@ def test_deferred_size_check_decision():
         g.ring_of(1)
 
 
+def test_world_of_one_direct_rank_exchanges_nothing(monkeypatch):
+    """A world of one rank that renders its bands straight into its frames (the one-GPU rehearsal of
+    the default N > 1 path) has nothing to ship: its batches issue no size reduce, gather or decode,
+    and every batch is final as traced.  With rank 0 through the codec (--rank0-codec) the exchange
+    is still issued."""
+    from raytracer_hip import tilecodec
+    from raytracer_hip.dist import TileBandGather
+    W, H, br, F = 64, 32, 8, 4
+    rb = RowBands(W, H, br, 0, 1)
+    g = TileBandGather(rb, "cpu", F, lambda n: tilecodec.layout(W, H, br, 1, n), None, None)
+    assert g.solo and g.direct
+
+    def no_exchange(*a, **k):
+        raise AssertionError("a world of one direct rank issued an exchange")
+    monkeypatch.setattr(g, "_size_reduce", no_exchange)
+    monkeypatch.setattr(g, "_gather", no_exchange)
+    monkeypatch.setattr(g, "_decode", no_exchange)
+    for _ in range(3 * F):
+        g.commit(None)
+    g.drain(None)
+    assert g.batch == 3 and g.decoded == 3 and g.bytes_sent == 0 and not g.provisional
+    assert g.ring_of(2) is g.frames[2]
+    codec = TileBandGather(rb, "cpu", F, lambda n: tilecodec.layout(W, H, br, 1, n), None, None, rank0_codec=True)
+    assert not codec.solo
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_gloo_timed_region_repeat_counts_one_attempt(tmp_path, world):
     """bench.py's N>1 timed region with a speculative gather forced too short (every rank repeats the
