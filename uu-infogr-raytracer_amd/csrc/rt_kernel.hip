@@ -1655,7 +1655,7 @@ struct DirectK {
     };
 };
 #ifndef RT_SINGLE_WPG
-#define RT_SINGLE_WPG 1
+#define RT_SINGLE_WPG 4
 #endif
 #ifndef RT_WPG_ALL
 #define RT_WPG_ALL 0
