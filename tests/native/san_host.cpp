@@ -363,6 +363,105 @@ void check_shadow_grid() {
     (void)checked;
 }
 
+// The merged pass's level-0 ball cull with hoisted light-independent terms (rt_kernel.hip
+// shadow_members_fast, after make_shadow_sphere): for random scenes and random "waves" -- up to 64 hit
+// points in a cluster of random spread (tight tiles, scattered deep levels), near sphere surfaces and on
+// grazing shadow lines -- a (sphere, light) pair the cull drops must leave every lane's binary32 shadow
+// ray unblocked.  The bound is computed as the device does it (float; the device's clen3 uses the
+// hardware sqrt, covered by the (1 + 2^-10) inflation of R).
+struct Ball {
+    float ox, oy, oz, R, omgn;
+    bool ok;
+};
+Ball make_ball(const std::vector<rt_vec3>& hp) {
+    Ball b{};
+    const rt_vec3 a = hp.front(), z = hp.back();
+    b.ox = (a.x + z.x) * 0.5f, b.oy = (a.y + z.y) * 0.5f, b.oz = (a.z + z.z) * 0.5f;
+    float e = 0.0f;
+    bool bad = false;
+    for (const rt_vec3& q : hp) {
+        const float dx = q.x - b.ox, dy = q.y - b.oy, dz = q.z - b.oz;
+        const float el = std::sqrt(dx * dx + dy * dy + dz * dz);
+        bad = bad || !(el < 0x1p40f);
+        e = std::max(e, el);
+    }
+    b.R = e * (1.0f + 0x1p-10f) + 0x1p-60f;
+    const float olen = std::sqrt(b.ox * b.ox + b.oy * b.oy + b.oz * b.oz);
+    b.omgn = 0x1p-18f * olen * (1.0f + 0x1p-10f);
+    b.ok = !bad && b.R < 0x1p38f && olen < 0x1p40f;
+    return b;
+}
+bool ball_keeps(const Ball& b, const DevSphereCull& c, const DevLight& l) {
+    const float wx = c.cx - b.ox, wy = c.cy - b.oy, wz = c.cz - b.oz;
+    const float dc = (std::fabs(wx) + std::fabs(wy) + std::fabs(wz)) * (1.0f + 0x1p-20f);
+    const float c1 = std::fabs(c.cx) + std::fabs(c.cy) + std::fabs(c.cz);
+    const float mgn = std::fmaf(0x1p-8f, dc + 3.0f * b.R, b.omgn + 0x1p-18f * c1);
+    const float T = b.R + c.rr + mgn;
+    const float T2 = T * T, nb = -(b.R + mgn);
+    const bool valid = b.ok && c.rr >= 0x1p-50f && dc >= 0x1p-30f && dc < 0x1p40f && c1 < 0x1p40f;
+    const bool l_ok = l.a >= 0x1p-40f && l.a <= 0x1p40f && l.a2 < INFINITY;
+    const float wu = std::fmaf(wz, l.uz, std::fmaf(wy, l.uy, wx * l.ux));
+    const float wv = std::fmaf(wz, l.vz, std::fmaf(wy, l.vy, wx * l.vx));
+    const float wa = std::fmaf(wz, l.az, std::fmaf(wy, l.ay, wx * l.ax));
+    const bool line = std::fmaf(wu, wu, wv * wv) > T2;
+    const bool behind = wa < nb;
+    return !(valid && l_ok && (line || behind));
+}
+
+void check_ball_cull() {
+    long culled = 0, pairs = 0;
+    for (int it = 0; it < 40; ++it) {
+        const float scale = it % 4 == 3 ? 1000.0f : it % 4 == 2 ? 30.0f : 1.0f;
+        const int S = 12 + (int)(next64() % 53), L = 1 + (int)(next64() % SHADOW_MERGE_L);
+        std::vector<rt_sphere> sph((size_t)S);
+        std::vector<rt_light> li((size_t)L);
+        for (rt_sphere& q : sph) {
+            q.center = v3(unif(-8, 8) * scale, unif(-1, 3) * scale, unif(2, 40) * scale);
+            q.radius = unif(0.05f, 1.5f) * scale;
+            q.material = material((int)(next64() % 5));
+        }
+        for (int j = 0; j < L; ++j) {
+            li[(size_t)j].position = v3(unif(-40, 40), unif(-5, 20), unif(-20, 40));
+            li[(size_t)j].intensity = 1.0f;
+            if (j == 1 && it % 3 == 0) li[(size_t)j].position = v3(unif(-40, 40), 1e-3f, unif(-1, 1));
+        }
+        rt_ctx ctx;
+        CHECK(rt_set_scene(&ctx, sph.data(), S, nullptr, 0, li.data(), L, v3(0.1f, 0.1f, 0.1f), 3) == RT_OK, "scene");
+        const SceneLayout& lay = ctx.layout;
+        const DevLight* dl = (const DevLight*)(lay.host_blob.data() + lay.off_li);
+        const DevSphereCull* dc = (const DevSphereCull*)(lay.host_blob.data() + lay.off_cull);
+        for (int wv = 0; wv < 300; ++wv) {
+            // a wave's hit points: a cluster around a point near a sphere surface, spread from 1e-4 to 10 units
+            const rt_sphere& s0 = sph[next64() % (size_t)S];
+            const double d0[3] = {unif(-1, 1), unif(-1, 1), unif(-1, 1)};
+            const double n0 = std::sqrt(d0[0] * d0[0] + d0[1] * d0[1] + d0[2] * d0[2]) + 1e-30;
+            const double rr0 = (double)s0.radius * (1.0 + unif(-1e-3f, 5e-2f));
+            const double cx = s0.center.x + rr0 * d0[0] / n0, cy = s0.center.y + rr0 * d0[1] / n0,
+                         cz = s0.center.z + rr0 * d0[2] / n0;
+            const double spread = std::pow(10.0, unif(-4.0f, 1.0f)) * scale;
+            const int k = 1 + (int)(next64() % 64);
+            std::vector<rt_vec3> hp((size_t)k);
+            for (rt_vec3& q : hp)
+                q = v3((float)(cx + spread * unif(-1, 1)), (float)(cy + spread * unif(-1, 1)), (float)(cz + spread * unif(-1, 1)));
+            const Ball b = make_ball(hp);
+            for (int j = 0; j < L; ++j)
+                for (int i = 0; i < S; ++i) {
+                    ++pairs;
+                    if (ball_keeps(b, dc[i], dl[j])) continue;
+                    ++culled;
+                    for (const rt_vec3& q : hp) {
+                        int col = 0;
+                        oracle_intersect_sphere(q, li[(size_t)j].position, sph[(size_t)i].center, sph[(size_t)i].radius,
+                                                0.001f, &col);
+                        CHECK(!col, "scene %d wave %d light %d: sphere %d culled but blocks (%a, %a, %a)", it, wv, j, i,
+                              q.x, q.y, q.z);
+                    }
+                }
+        }
+    }
+    std::printf("ball_cull: %ld of %ld (sphere, light) pairs culled, every lane checked unblocked\n", culled, pairs);
+}
+
 void check_library() {
     CHECK(rt_abi_version() == RT_ABI_VERSION, "ABI version");
     int n = -1;
@@ -386,6 +485,7 @@ int main() {
     check_wire_layout();
     check_shadow_threshold();
     check_shadow_grid();
+    check_ball_cull();
     std::printf("san_host: %d failures\n", failures);
     return failures ? 1 : 0;
 }

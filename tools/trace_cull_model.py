@@ -34,9 +34,10 @@ def walk(sc, xs, ys):
     n = len(xs)
     active = np.ones(n, bool)
     segs = []
+    prev = np.full(n, -1)
     for count in range(sc.recursion_limit + 1):
         if count > 0:
-            segs.append((o.copy(), d.copy(), active.copy()))
+            segs.append((o.copy(), d.copy(), active.copy(), prev.copy()))
         oc = o[:, None, :] - C[None]
         b = 2 * np.einsum("nsk,nk->ns", oc, d)
         c = np.einsum("nsk,nsk->ns", oc, oc) - r2[None]
@@ -61,6 +62,7 @@ def walk(sc, xs, ys):
         nrm = np.where(is_s[:, None], nrm / np.maximum(np.linalg.norm(nrm, axis=1, keepdims=True), 1e-30), nrm)
         d = d - nrm * (2 * np.einsum("nk,nk->n", d, nrm))[:, None]
         o = hp
+        prev = np.where(is_s, si, -1 - pi)
         active = mirror
         if not active.any():
             break
@@ -108,26 +110,34 @@ def main():
     TX, TY = [v.ravel() for v in np.meshgrid(tx, ty, indexing="ij")]
     lane = np.arange(64)
     L = sc.recursion_limit
-    cnt = np.zeros((L + 1, 4))  # waves, active lanes, bundle candidates, reachable
+    cnt = np.zeros((L + 1, 6))  # waves, active lanes, bundle candidates, reachable, split by previous primitive, groups
     for c0 in range(0, len(TX), 1024):
         xs = (TX[c0:c0 + 1024, None] * 8 + (lane & 7)[None]).ravel().astype(float)
         ys = (TY[c0:c0 + 1024, None] * 8 + (lane >> 3)[None]).ravel().astype(float)
-        for k, (o, d, act) in enumerate(walk(sc, xs, ys), start=1):
-            o, d, act = o.reshape(-1, 64, 3), d.reshape(-1, 64, 3), act.reshape(-1, 64)
+        for k, (o, d, act, pv) in enumerate(walk(sc, xs, ys), start=1):
+            o, d, act, pv = o.reshape(-1, 64, 3), d.reshape(-1, 64, 3), act.reshape(-1, 64), pv.reshape(-1, 64)
             for w in range(o.shape[0]):
                 m = act[w]
                 if not m.any():
                     continue
-                cnt[k] += (1, m.sum(), bundle_cull(o[w][m], d[w][m], C, rr).sum(), reachable(o[w][m], d[w][m], C, r2).sum())
+                # split: the lanes that reflected off the first active lane's primitive, then the rest
+                first = pv[w][m][0]
+                g1 = m & (pv[w] == first)
+                g2 = m & ~g1
+                split = bundle_cull(o[w][g1], d[w][g1], C, rr).sum() + (
+                    bundle_cull(o[w][g2], d[w][g2], C, rr).sum() if g2.any() else 0)
+                cnt[k] += (1, m.sum(), bundle_cull(o[w][m], d[w][m], C, rr).sum(), reachable(o[w][m], d[w][m], C, r2).sum(),
+                           split, 1 + g2.any())
     print(f"# {sc.name}: {len(TX)} sampled waves; per reflected segment k: waves with active lanes per sampled wave, "
           f"active lanes, bundle candidates, reachable spheres (per such wave)")
     for k in range(1, L + 1):
         if cnt[k, 0]:
             n = cnt[k, 0]
             print(f"  k={k}: waves {n / len(TX):.3f}  lanes {cnt[k, 1] / n:5.1f}  bundle cands {cnt[k, 2] / n:5.2f}  "
-                  f"reachable {cnt[k, 3] / n:5.2f}")
+                  f"reachable {cnt[k, 3] / n:5.2f}  split-by-prev-prim cands {cnt[k, 4] / n:5.2f} (groups {cnt[k, 5] / n:4.2f})")
     tot = cnt[1:].sum(axis=0)
-    print(f"  per sampled wave: bundle candidates {tot[2] / len(TX):.2f}, reachable {tot[3] / len(TX):.2f}")
+    print(f"  per sampled wave: bundle candidates {tot[2] / len(TX):.2f}, reachable {tot[3] / len(TX):.2f}, "
+          f"split {tot[4] / len(TX):.2f} in {tot[5] / len(TX):.2f} bundles")
 
 
 if __name__ == "__main__":

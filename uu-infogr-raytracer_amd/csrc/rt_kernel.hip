@@ -1160,6 +1160,44 @@ __device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d,
 // for light li (lights some lane wants only).  Converged call.  (Hoisting the light-independent
 // terms of the cull out of the light loop cut VALU 1.8 % but spilled 12 B/lane: C4 +0.8 %, C5 +0.8 %,
 // profiles/ab/r03_shadow_queue_rejected.txt.)
+// shadow_members with the light-independent terms hoisted out of the light loop (the merged
+// instantiation, whose register budget has room for them; RT_FAST_MEMBERS): lane i loads sphere
+// i's centre and r' once, w = C - O, the world-frame L1 bound dc >= |C - O| and the threshold T of
+// the line rule once, and per light only projects w onto (U, V, A) -- FMA allowed, culling only --
+// and applies the same two rules: line miss if |w_perp|^2 > T^2, behind if w.A < -(R + mgn).  The
+// margins are shadow_sphere_cull's: 2^-8 (dc + 3R) with dc from the unprojected w, plus 2^-18
+// (|O| + |C|_1) for the rounding of w and of its projections (each < 2^-21 |w|_1, far inside).
+#ifndef RT_FAST_MEMBERS
+#define RT_FAST_MEMBERS 1
+#endif
+__device__ __forceinline__ unsigned shadow_members_fast(const LaunchParams& p, const ShadowSphere& SS, unsigned want) {
+    const int lane = threadIdx.x & 63;
+    const bool in = lane < p.S;
+    const DevSphereCull c = p.scull[in ? lane : 0];
+    const f3 w = sub(mk(c.cx, c.cy, c.cz), SS.O);
+    const float dc = (__builtin_fabsf(w.x) + __builtin_fabsf(w.y) + __builtin_fabsf(w.z)) * (1.0f + 0x1p-20f);
+    const float c1 = __builtin_fabsf(c.cx) + __builtin_fabsf(c.cy) + __builtin_fabsf(c.cz);
+    const float mgn = __builtin_fmaf(0x1p-8f, dc + 3.0f * SS.R, SS.omgn + 0x1p-18f * c1);
+    const float T = SS.R + c.rr + mgn;
+    const float T2 = T * T, nb = -(SS.R + mgn);
+    // NaN anywhere -> candidate; a ball that allows no culling keeps every sphere
+    const bool valid = SS.ok && p.shcull != nullptr && c.rr >= 0x1p-50f && dc >= 0x1p-30f && dc < 0x1p40f &&
+                       c1 < 0x1p40f;
+    unsigned memb = 0;
+    for (int li = 0; li < p.L; ++li) {
+        if (__builtin_amdgcn_ballot_w64((want >> li) & 1u) == 0) continue;  // wave-uniform
+        const DevLight& l = p.li[li];
+        const bool l_ok = l.a >= 0x1p-40f && l.a <= 0x1p40f && l.a2 < __builtin_inff();  // wave-uniform
+        const float wu = __builtin_fmaf(w.z, l.uz, __builtin_fmaf(w.y, l.uy, w.x * l.ux));
+        const float wv = __builtin_fmaf(w.z, l.vz, __builtin_fmaf(w.y, l.vy, w.x * l.vx));
+        const float wa = __builtin_fmaf(w.z, l.az, __builtin_fmaf(w.y, l.ay, w.x * l.ax));
+        const bool line = __builtin_fmaf(wu, wu, wv * wv) > T2;
+        const bool behind = wa < nb;
+        const bool cull = valid & l_ok & (line | behind);
+        memb |= (in & !cull) ? (1u << li) : 0u;
+    }
+    return memb;
+}
 __device__ __forceinline__ unsigned shadow_members(const LaunchParams& p, const ShadowSphere& SS, unsigned want) {
     const int lane = threadIdx.x & 63;
     unsigned memb = 0;
@@ -1299,7 +1337,9 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
         // level 0 (the tile's primary hits, coherent) one bound around them culls tighter than the
         // grid's cells (wave-uniform choice)
         const unsigned memb = (p.shg && level >= RT_GRID_FROM_LEVEL) ? shadow_members_grid(p, hp, want)
-                                                                      : shadow_members(p, make_shadow_sphere(hp, diff), want);
+                                                                      : RT_FAST_MEMBERS
+                                                                            ? shadow_members_fast(p, make_shadow_sphere(hp, diff), want)
+                                                                            : shadow_members(p, make_shadow_sphere(hp, diff), want);
         blk = shadow_merged(p, memb, hp, want, diff, act, tl);
     }
     f3 normal;
