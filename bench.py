@@ -1055,6 +1055,13 @@ def main_single(args, torch, Context, abi, scenes):
             out["also"][sc2.name] = {k: r2[k] for k in ("value", "unit", "ms_per_step", "fps", "rays_per_frame",
                                                         "workload", "kernel", "kernel_avg_ms", "kernel_ms_per_frame",
                                                         "frames_per_launch", "launches", "hbm_frac")}
+            # VALU issue (the binding resource) from the committed PMC summary of this config, as for the line
+            pmc2 = load_pmc(args.pmc, sc2.name, 1)
+            v2 = (pmc2.get("counters") or {}).get("SQ_INSTS_VALU") if pmc2 else None
+            if v2:
+                per_frame = v2 / (pmc2.get("frames_per_launch") or 1)
+                out["also"][sc2.name]["valu_frac"] = (per_frame * 64 / (r2["kernel_ms_per_frame"] / 1e3) / 1e12
+                                                      / VALU_PEAK_TOPS)
     if not args.no_cpu_baseline:
         # the bench config, then C3 (the north-star config: 1080p with reflections), C1
         # (BASELINE configs[0]) and the verbatim reference scene beside it
