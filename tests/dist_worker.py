@@ -293,8 +293,8 @@ def run_timed_attempts(rank, world, port, result_path):
             ctx.rays += rays_per_attempt
             size = torch.tensor([500 + 400 * rank], dtype=torch.int64)  # this rank's wire
             dist.all_reduce(size, op=dist.ReduceOp.MAX)
-            if tg.defer_checks:  # speculative: ships 600 bytes, the size is checked afterwards
-                tg.size_host[0] = int(size)
+            if tg.defer_checks:  # speculative: ships 600 bytes, the size is reduced and checked afterwards
+                tg.size[0].fill_(500 + 400 * rank)  # this rank's wire; check_deferred reduces the maximum
                 tg.provisional.add(tg.batch)
                 tg.pending_checks.append((tg.batch, steps, 600, 0))
                 tg.bytes_sent += 600

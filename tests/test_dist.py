@@ -176,13 +176,15 @@ def test_deferred_size_check_decision():
     from raytracer_hip.dist import TileBandGather
     W, H, br = 64, 32, 8
     rb = RowBands(W, H, br, 0, 1)
+    from raytracer_hip.dist import _Done
     g = TileBandGather(rb, "cpu", 4, lambda n: tilecodec.layout(W, H, br, 1, n), None, None, rank0_codec=True)
+    g._size_reduce = lambda i: _Done()  # (world of one: the maximum over ranks is the rank's own size)
     g.provisional.update({0, 1})
     g.pending_checks = [(0, 4, 800, 0)]
-    g.size_host[0] = 790  # rounded up to 792 <= 800: the gather sufficed
+    g.size[0].fill_(790)  # rounded up to 792 <= 800: the gather sufficed
     assert g.check_deferred() is True and 0 not in g.provisional and g.redone == 0
     g.pending_checks = [(1, 4, 800, 1)]
-    g.size_host[1] = 801
+    g.size[1].fill_(801)
     assert g.check_deferred() is False and 1 not in g.provisional and 1 in g.abandoned
     assert g.redone == 0 and g.deferred_failed == 1
     assert g.pending_checks == [] and g.max_per_frame == 808 / 4

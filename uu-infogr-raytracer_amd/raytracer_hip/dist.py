@@ -498,10 +498,12 @@ class TileBandGather:
         if first:
             # the gather right behind the encode and the size reduce after it, so that neither the
             # reduce nor its read-back sits between the encode and the decode: stage C decodes, then
-            # checks the reduced size (and gathers + decodes again if it was exceeded)
+            # checks the reduced size (and gathers + decodes again if it was exceeded).  A deferred
+            # check (defer_checks, GPUs) reduces the size only after the caller's region has ended
+            # (check_deferred): no collective between this batch's gather and its decode at all
             n = self._spec_bytes(n_frames)
             gw = self._gather(b, i, n)
-            work = self._size_reduce(i)
+            work = None if (self.defer_checks and self.cuda) else self._size_reduce(i)
             self.stage_c.append((b, n_frames, gw, (work, n, True)))
         else:
             work = self._size_reduce(i)
@@ -537,12 +539,7 @@ class TileBandGather:
                 self.provisional.add(b)
                 self._decode(b, n_frames, gw)
             if decode_first and self.defer_checks and self.cuda:
-                import torch
-                i = b % 3
-                with torch.cuda.stream(self.comm):  # after the size reduce, no host wait
-                    work.wait()
-                    self.size_host[i:i + 1].copy_(self.size[i], non_blocking=True)
-                self.pending_checks.append((b, n_frames, n_spec, i))
+                self.pending_checks.append((b, n_frames, n_spec, b % 3))  # size reduced in check_deferred
                 self.bytes_sent += n_spec
                 if self.root:
                     self.decoded += 1
@@ -561,13 +558,15 @@ class TileBandGather:
             self.decoded += 1
 
     def check_deferred(self):
-        """After the caller's device synchronisation: the deferred size checks (defer_checks).  Returns
+        """After the caller's device synchronisation, on every rank: the deferred size checks
+        (defer_checks) -- each batch's size reduce is issued here, outside the caller's region.  Returns
         True when every speculative gather sufficed (the batches are final); False when some wire
         outgrew its gather (every rank sees the same reduced size, so every rank returns the same) --
         those batches stay provisional and the run must be repeated without speculation."""
         ok = True
         for b, n_frames, n_spec, i in self.pending_checks:
-            n = (int(self.size_host[i]) + 7) // 8 * 8
+            # the wire sizes' maximum over ranks (collective: every rank checks alike), then read back
+            n = self._read_size(i, self._size_reduce(i))
             self.max_per_frame = max(self.max_per_frame, n / n_frames)
             if n > n_spec:
                 ok = False
