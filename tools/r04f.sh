@@ -18,3 +18,4 @@ for cfg in C2 C4; do
     cat gpurun_out/dtrace_${cfg}_reconcile.txt
 done
 for cfg in C2 C3 C4 C5; do cat gpurun_out/trace_${cfg}_reconcile.txt; done
+bash tools/r04h.sh > gpurun_out/r04h.log 2>&1 || { tail -20 gpurun_out/r04h.log; exit 1; }
