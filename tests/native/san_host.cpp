@@ -462,6 +462,28 @@ void check_ball_cull() {
     std::printf("ball_cull: %ld of %ld (sphere, light) pairs culled, every lane checked unblocked\n", culled, pairs);
 }
 
+// Single-frame row order (rows_cost_low): a floor below the camera fills the bottom rows (high y),
+// so they are dispatched first; a ceiling above it keeps the natural order; no visible plane and no
+// spheres: uniform cost, natural order.
+void check_row_order() {
+    for (int k = 0; k < 3; ++k) {
+        rt_ctx ctx;
+        rt_plane pl{};
+        pl.center = v3(0, k == 0 ? -1.0f : 1.0f, 0);
+        pl.normal = v3(0, k == 0 ? 1.0f : -1.0f, 0);
+        pl.material = material(0);
+        rt_light l{v3(0, 5, 0), 1.0f};
+        CHECK(rt_set_scene(&ctx, nullptr, 0, &pl, k == 2 ? 0 : 1, &l, 1, v3(0.1f, 0.1f, 0.1f), 1) == RT_OK, "scene");
+        rt_camera cam{v3(0, 0, 0), 0, 0};
+        rt_set_camera(&ctx, &cam);
+        LaunchParams lp;
+        std::memset(&lp, 0, sizeof lp);
+        CHECK(view_params(&ctx, 1920, 1080, lp) == RT_OK, "view_params");
+        CHECK(lp.row_rev == (k == 0 ? 1 : 0), "row order %d for %s", lp.row_rev,
+              k == 0 ? "a floor" : k == 1 ? "a ceiling" : "an empty scene");
+    }
+}
+
 void check_library() {
     CHECK(rt_abi_version() == RT_ABI_VERSION, "ABI version");
     int n = -1;
@@ -486,6 +508,7 @@ int main() {
     check_shadow_threshold();
     check_shadow_grid();
     check_ball_cull();
+    check_row_order();
     std::printf("san_host: %d failures\n", failures);
     return failures ? 1 : 0;
 }

@@ -162,6 +162,7 @@ struct SceneLayout {
     std::vector<unsigned char> host_blob;  // the uploaded scene image (host tests read the tables)
     bool generic_pow = false;        // a specular material with n not in {0.5, 1, 2}
     std::vector<DevSphere> host_sph;  // for the per-frame primary constants
+    std::vector<DevPlane> host_pl;    // for the single-frame launches' row order (rows_cost_low)
 };
 }  // namespace
 
@@ -394,6 +395,42 @@ PrimBox prim_box(const LaunchParams& lp, const DevSphere& s) {
     return b;
 }
 
+// Order of a single-frame launch's tile rows (LaunchParams::row_rev).  The launch's last waves set its
+// tail, so the expensive rows should start first.  The cost of a tile row is estimated from three
+// primary rays (columns W/6, W/2, 5W/6 of its middle pixel row): 1 per ray, plus 1 + L when the ray
+// meets a plane in front of the camera or falls inside a sphere's screen box (prim_box) -- a hit gets
+// shaded, with shadow rays.  Reverse when the cost's centre of mass lies in the lower half.  The
+// estimate only orders the workgroups: every tile is traced exactly as before.
+bool rows_cost_low(const LaunchParams& lp, const SceneLayout& L) {
+    const int rows = (lp.H + 7) / 8;
+    if (rows < 2) return false;
+    double mass = 0, moment = 0;
+    const int cols[3] = {lp.W / 6, lp.W / 2, (5 * lp.W) / 6};
+    for (int r = 0; r < rows; ++r) {
+        const int y = std::min(lp.H - 1, r * 8 + 4);
+        const double ly = ((double)y / lp.H - 0.5) * lp.ph;
+        double c = 0;
+        for (int x : cols) {
+            const double lx = ((double)x / lp.W - 0.5) * lp.pw;
+            double d[3];
+            for (int k = 0; k < 3; ++k) d[k] = lp.right[k] * lx + lp.up[k] * ly + lp.fwd[k] * lp.nearc;
+            bool hit = false;
+            for (const DevPlane& q : L.host_pl) {
+                const double den = d[0] * q.nx + d[1] * q.ny + d[2] * q.nz;
+                const double num = q.cn - (lp.cam[0] * q.nx + lp.cam[1] * q.ny + lp.cam[2] * q.nz);
+                if (den != 0 && num / den > 0) hit = true;
+            }
+            if (lp.prim_const)
+                for (size_t i = 0; i < L.host_sph.size() && !hit; ++i)
+                    hit = x >= lp.pbox[i].x0 && x <= lp.pbox[i].x1 && y >= lp.pbox[i].y0 && y <= lp.pbox[i].y1;
+            c += 1.0 + (hit ? 1.0 + L.L : 0.0);
+        }
+        mass += c;
+        moment += c * r;
+    }
+    return moment / mass > 0.5 * (rows - 1);
+}
+
 void copy_view(const LaunchParams& from, LaunchParams& to) {
     std::memcpy(to.cam, from.cam, sizeof to.cam);
     std::memcpy(to.right, from.right, sizeof to.right);
@@ -404,6 +441,7 @@ void copy_view(const LaunchParams& from, LaunchParams& to) {
     to.prim_const = from.prim_const;
     std::memcpy(to.pc, from.pc, sizeof to.pc);
     std::memcpy(to.pbox, from.pbox, sizeof to.pbox);
+    to.row_rev = from.row_rev;
 }
 
 int view_params(rt_ctx* ctx, int W, int H, LaunchParams& lp) {
@@ -430,6 +468,9 @@ int view_params(rt_ctx* ctx, int W, int H, LaunchParams& lp) {
             lp.pc[i] = PrimConst{oc.x, oc.y, oc.z, hdot(oc, oc) - sph[i].r2};
             lp.pbox[i] = prim_box(lp, sph[i]);
         }
+    // RT_ROW_ORDER=0: natural row order for single-frame launches (A/B)
+    const char* ro = std::getenv("RT_ROW_ORDER");
+    lp.row_rev = (ro && ro[0] == '0') ? 0 : rows_cost_low(lp, ctx->layout) ? 1 : 0;
     copy_view(lp, ctx->view_lp);
     ctx->view_cam = ctx->cam, ctx->view_w = W, ctx->view_h = H, ctx->view_ok = true;
     return RT_OK;
@@ -880,6 +921,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
         pl[i] = d;
         mat[n_spheres + i] = dev_material(p.material, ambient);
     }
+    L.host_pl.assign(pl, pl + n_planes);
     std::vector<Frame3> frames((size_t)n_lights);
     for (int i = 0; i < n_lights; ++i) {
         const rt_light& l = lights[i];

@@ -150,6 +150,9 @@ struct LaunchParams {
     // global row = band * band_rows + r % band_rows; pixel written at out[r * W + x].
     int band_rows, band_first, band_step, local_rows;
     int n_frames;  // grid z (frames of one batch launch, all with this view); 0 = 1
+    int row_rev;   // single-frame launches: tile rows dispatched last row first (the host's cost
+                   // estimate puts the expensive rows at the bottom: they start first, the cheap ones
+                   // fill the launch's tail)
     int32_t* out;
     unsigned long long out_frame_bytes;  // batch launches: frame z of the grid at (char*)out + z * out_frame_bytes
     int out_fmt;  // 0: int32 0x00RRGGBB per pixel; 1: packed 24-bit (bytes B, G, R); 2: int32 at frame row y;

@@ -767,10 +767,10 @@ __device__ __forceinline__ Hit terminal_direct(const LaunchParams& p, f3 o, f3 d
 // DIRECT path, one 8x8 tile: each lane walks its own chain with per-lane (divergent) control
 // flow.  Returns the lane's packed counts: reflected segments (bits 0-7) | shadow rays << 8.
 template <int K, bool GPOW, bool TILES, typename T>
-__device__ __forceinline__ unsigned trace_tile_direct(const LaunchParams& p, int tile_x, float2* stk_lv, float* stk_dv,
-                                                      T& tl) {
+__device__ __forceinline__ unsigned trace_tile_direct(const LaunchParams& p, int tile_x, int tile_y, float2* stk_lv,
+                                                      float* stk_dv, T& tl) {
     const int lane = threadIdx.x & 63;
-    const TilePixel tpx = tile_pixel(p, tile_x * TILE_W + (lane & 7), blockIdx.y * TILE_H + (lane >> 3));
+    const TilePixel tpx = tile_pixel(p, tile_x * TILE_W + (lane & 7), tile_y * TILE_H + (lane >> 3));
     const int x = tpx.x, r = tpx.r, y = tpx.y;
     const bool valid = tpx.valid;
     const unsigned long long pmask = p.prim_const ? prim_box_mask(p, x, y) : 0;
@@ -856,7 +856,9 @@ __global__ __launch_bounds__(WG_THREADS * WPG) void trace_direct_kernel(LaunchPa
     const int wave = WPG > 1 ? (int)(threadIdx.x >> 6) : 0;
     float2* lv = stk_lv + (LDS_LEVELS > 0 ? wave * LDS_LEVELS * WG_THREADS : 0);
     float* dv = stk_dv + (LDS_LEVELS > 0 ? wave * 3 * WG_THREADS : 0);
-    const unsigned cnt = trace_tile_direct<K, GPOW, TILES>(p, (int)blockIdx.x * WPG + wave, lv, dv, tl);
+    // single-frame launches: the host may reverse the tile-row order (LaunchParams::row_rev)
+    const int tile_y = WPG > 1 && p.row_rev ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
+    const unsigned cnt = trace_tile_direct<K, GPOW, TILES>(p, (int)blockIdx.x * WPG + wave, tile_y, lv, dv, tl);
     add_counters<STATS>(p, threadIdx.x & 63, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
 }
 
