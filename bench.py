@@ -370,11 +370,13 @@ def single_summary(sc, m, steps):
     }
 
 
-def tick_rates(ctx, W, H, torch, n=20, reps=3):
+def tick_rates(ctx, W, H, torch, n=20, reps=3, n_single=200):
     """The interactive shapes beside the batched headline (never `value`); each the median of
     `reps` runs of n frames, same camera:
     - single_launch_fps: rt_render_device, one frame per launch, device-resident (what a Tick()
-      loop issues, without the PCIe hand-off);
+      loop issues, without the PCIe hand-off), over runs of n_single frames: a display loop's
+      steady rate (single_launch_fps_20: runs of 20, where the first launch's start and the closing
+      synchronisation, ~50 us together, are spread over 20 frames only);
     - tick_fps_incl_d2h: rt_render, the synchronous Tick() (trace + D2H into the caller's
       registered buffer, returns with the frame complete);
     - tick_async_fps_incl_d2h: rt_render_async into two alternating registered buffers and an
@@ -383,22 +385,24 @@ def tick_rates(ctx, W, H, torch, n=20, reps=3):
     rt_render_async's D2H of frame k rides in frame k+1's launch (copy slice) or rt_wait's."""
     import numpy as np
 
-    def med(fn):
+    def med(fn, frames=n):
         fn()  # warm
         rates = []
         for _ in range(reps):
             t = time.perf_counter()
             fn()
-            rates.append(n / (time.perf_counter() - t))
+            rates.append(frames / (time.perf_counter() - t))
         return sorted(rates)[len(rates) // 2], [round(r, 1) for r in rates]
 
     dev = torch.empty(W * H, dtype=torch.int32, device="cuda")
     st = torch.cuda.current_stream()
 
-    def single():
-        for _ in range(n):
-            ctx.render_device(W, H, dev.data_ptr(), st.cuda_stream)
-        torch.cuda.synchronize()
+    def single_of(frames):
+        def run():
+            for _ in range(frames):
+                ctx.render_device(W, H, dev.data_ptr(), st.cuda_stream)
+            torch.cuda.synchronize()
+        return run
     hosts = [np.zeros(W * H, dtype=np.int32) for _ in range(n)]
     for hb in hosts:
         ctx.register_host(hb)
@@ -419,13 +423,15 @@ def tick_rates(ctx, W, H, torch, n=20, reps=3):
             ctx.render_async(W, H, hosts[k])
         ctx.wait()
     out = {}
-    for key, fn in (("single_launch_fps", single), ("tick_fps_incl_d2h", sync), ("tick_async_fps_incl_d2h", pair),
-                    ("tick_async_deep_fps_incl_d2h", deep)):
+    out["single_launch_fps"], out["single_launch_fps_runs"] = med(single_of(n_single), n_single)
+    for key, fn in (("single_launch_fps_20", single_of(n)), ("tick_fps_incl_d2h", sync),
+                    ("tick_async_fps_incl_d2h", pair), ("tick_async_deep_fps_incl_d2h", deep)):
         out[key], out[key + "_runs"] = med(fn)
     for hb in hosts:
         ctx.unregister_host(hb)
-    out["tick_note"] = (f"median of {reps} runs of {n} frames each; single_launch_fps = rt_render_device one frame per "
-                        f"launch into HBM; tick_* include the D2H into registered host memory (PCIe)")
+    out["tick_note"] = (f"median of {reps} runs each; single_launch_fps = rt_render_device one frame per launch into "
+                        f"HBM, runs of {n_single} frames (single_launch_fps_20: runs of {n}); tick_* runs of {n} "
+                        f"frames, including the D2H into registered host memory (PCIe)")
     return out
 
 
