@@ -108,6 +108,15 @@ void check_scene_packing() {
             rc = view_params(&ctx, W, H, lp);
             CHECK(rc == RT_OK, "view_params rc %d", rc);
             CHECK(lp.prim_const == (S <= MAX_PRIM_CONST ? 1 : 0), "prim_const flag");
+            // the single-frame row order is a permutation of the frame's tile rows (or absent)
+            const int rows = (H + 7) / 8;
+            CHECK(lp.row_order_n == 0 || lp.row_order_n == rows, "row order over %d of %d rows", lp.row_order_n, rows);
+            CHECK(lp.row_order_n > 0 || rows < 2 || rows > ROW_ORDER_MAX, "no row order for %d rows", rows);
+            std::vector<char> seen((size_t)rows, 0);
+            for (int r = 0; r < lp.row_order_n; ++r) {
+                CHECK(lp.row_order[r] < rows && !seen[lp.row_order[r]], "row order not a permutation at %d", r);
+                if (lp.row_order[r] < rows) seen[lp.row_order[r]] = 1;
+            }
             // a box is never empty: the sphere is strictly in front (cz > rho), so both tangent
             // directions lie in (-pi/2, pi/2) and tan keeps their order
             for (int i = 0; lp.prim_const && i < S; ++i)
@@ -462,9 +471,9 @@ void check_ball_cull() {
     std::printf("ball_cull: %ld of %ld (sphere, light) pairs culled, every lane checked unblocked\n", culled, pairs);
 }
 
-// Single-frame row order (rows_cost_low): a floor below the camera fills the bottom rows (high y),
-// so they are dispatched first; a ceiling above it keeps the natural order; no visible plane and no
-// spheres: uniform cost, natural order.
+// Single-frame row order (row_order): a floor below the camera fills the bottom rows (high y), so they
+// are dispatched first; a ceiling above it puts the top rows first; with no plane and no sphere every
+// row costs the same and the order stays natural.
 void check_row_order() {
     for (int k = 0; k < 3; ++k) {
         rt_ctx ctx;
@@ -479,8 +488,11 @@ void check_row_order() {
         LaunchParams lp;
         std::memset(&lp, 0, sizeof lp);
         CHECK(view_params(&ctx, 1920, 1080, lp) == RT_OK, "view_params");
-        CHECK(lp.row_rev == (k == 0 ? 1 : 0), "row order %d for %s", lp.row_rev,
-              k == 0 ? "a floor" : k == 1 ? "a ceiling" : "an empty scene");
+        CHECK(lp.row_order_n == 135, "row order over %d rows", lp.row_order_n);
+        if (k == 0) CHECK(lp.row_order[0] >= 68 && lp.row_order[134] <= 67, "floor: bottom rows first (%d ... %d)", lp.row_order[0], lp.row_order[134]);
+        if (k == 1) CHECK(lp.row_order[0] < 67 && lp.row_order[134] >= 67, "ceiling: top rows first (%d ... %d)", lp.row_order[0], lp.row_order[134]);
+        if (k == 2)
+            for (int r = 0; r < 135; ++r) CHECK(lp.row_order[r] == r, "empty scene: natural order at %d", r);
     }
 }
 

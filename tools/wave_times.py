@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--batch", type=int, default=1, help="frames per launch (1: the single-frame launch)")
     ap.add_argument("--reps", type=int, default=5, help="launches analysed (each the last of a back-to-back run)")
     ap.add_argument("--map", action="store_true", help="print a coarse map of wave durations")
+    ap.add_argument("--save", default="", help="write the last launch's per-tile start / duration (us) to this .npz")
     a = ap.parse_args()
     import torch
     from raytracer_hip import Context, abi, scenes
@@ -71,6 +72,8 @@ def main():
                          end90=pct(end, 90) * TICK_US, end99=pct(end, 99) * TICK_US, dur50=pct(dur, 50) * TICK_US,
                          dur99=pct(dur, 99) * TICK_US, durmax=dur.max() * TICK_US, cus=ncu, idle_tail=idle_tail * TICK_US,
                          work=float(dur.sum()) * TICK_US))
+        if rep == a.reps - 1 and a.save:
+            np.savez(a.save, start=start * TICK_US, dur=dur * TICK_US, tiles_x=tx, tiles_y=ty)
         if rep == a.reps - 1:
             order = np.argsort(-end)[:12]
             print(f"# {a.config} {W}x{H} batch={a.batch}: {n} waves on {ncu} CUs; the 12 last to finish "

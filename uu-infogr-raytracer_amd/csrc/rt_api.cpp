@@ -162,7 +162,7 @@ struct SceneLayout {
     std::vector<unsigned char> host_blob;  // the uploaded scene image (host tests read the tables)
     bool generic_pow = false;        // a specular material with n not in {0.5, 1, 2}
     std::vector<DevSphere> host_sph;  // for the per-frame primary constants
-    std::vector<DevPlane> host_pl;    // for the single-frame launches' row order (rows_cost_low)
+    std::vector<DevPlane> host_pl;    // for the single-frame launches' row order (row_order)
 };
 }  // namespace
 
@@ -395,40 +395,47 @@ PrimBox prim_box(const LaunchParams& lp, const DevSphere& s) {
     return b;
 }
 
-// Order of a single-frame launch's tile rows (LaunchParams::row_rev).  The launch's last waves set its
-// tail, so the expensive rows should start first.  The cost of a tile row is estimated from three
-// primary rays (columns W/6, W/2, 5W/6 of its middle pixel row): 1 per ray, plus 1 + L when the ray
-// meets a plane in front of the camera or falls inside a sphere's screen box (prim_box) -- a hit gets
-// shaded, with shadow rays.  Reverse when the cost's centre of mass lies in the lower half.  The
-// estimate only orders the workgroups: every tile is traced exactly as before.
-bool rows_cost_low(const LaunchParams& lp, const SceneLayout& L) {
+// Order of a single-frame launch's tile rows (LaunchParams::row_order).  The launch's last waves set
+// its tail, so the expensive rows should start first and the cheap ones come last.  A tile row's cost
+// is estimated from eight primary rays through its middle pixel row: 1 for a ray that meets nothing,
+// 1 + L when it meets a plane in front of the camera or falls inside a diffuse sphere's screen box
+// (prim_box: shaded, with shadow rays), (1 + L)(1 + min(limit, 4)) inside a mirror sphere's box (its
+// reflected chain is shaded too).  Rows are sorted by decreasing estimate, ties in natural order.
+// The estimate only orders the workgroups: every tile is traced exactly as before.
+int row_order(const LaunchParams& lp, const SceneLayout& L, uint16_t* order) {
     const int rows = (lp.H + 7) / 8;
-    if (rows < 2) return false;
-    double mass = 0, moment = 0;
-    const int cols[3] = {lp.W / 6, lp.W / 2, (5 * lp.W) / 6};
+    if (rows < 2 || rows > ROW_ORDER_MAX) return 0;
+    const DevMaterial* mat = L.host_blob.size() >= L.off_mat + sizeof(DevMaterial) * (size_t)(L.S + L.P)
+                                 ? (const DevMaterial*)(L.host_blob.data() + L.off_mat)
+                                 : nullptr;
+    const double shade = 1.0 + L.L, mirror = shade * (1.0 + std::min(L.limit, 4));
+    std::vector<double> cost((size_t)rows, 0.0);
     for (int r = 0; r < rows; ++r) {
         const int y = std::min(lp.H - 1, r * 8 + 4);
         const double ly = ((double)y / lp.H - 0.5) * lp.ph;
-        double c = 0;
-        for (int x : cols) {
+        for (int j = 0; j < 8; ++j) {
+            const int x = (int)(((2 * j + 1) * (long long)lp.W) / 16);
             const double lx = ((double)x / lp.W - 0.5) * lp.pw;
             double d[3];
             for (int k = 0; k < 3; ++k) d[k] = lp.right[k] * lx + lp.up[k] * ly + lp.fwd[k] * lp.nearc;
-            bool hit = false;
+            double w = 1.0;
             for (const DevPlane& q : L.host_pl) {
                 const double den = d[0] * q.nx + d[1] * q.ny + d[2] * q.nz;
                 const double num = q.cn - (lp.cam[0] * q.nx + lp.cam[1] * q.ny + lp.cam[2] * q.nz);
-                if (den != 0 && num / den > 0) hit = true;
+                if (den != 0 && num / den > 0) w = std::max(w, shade);
             }
             if (lp.prim_const)
-                for (size_t i = 0; i < L.host_sph.size() && !hit; ++i)
-                    hit = x >= lp.pbox[i].x0 && x <= lp.pbox[i].x1 && y >= lp.pbox[i].y0 && y <= lp.pbox[i].y1;
-            c += 1.0 + (hit ? 1.0 + L.L : 0.0);
+                for (int i = 0; i < L.S; ++i)
+                    if (x >= lp.pbox[i].x0 && x <= lp.pbox[i].x1 && y >= lp.pbox[i].y0 && y <= lp.pbox[i].y1)
+                        w = std::max(w, mat && (mat[i].flags & MAT_MIRROR) ? mirror : shade);
+            cost[(size_t)r] += w;
         }
-        mass += c;
-        moment += c * r;
     }
-    return moment / mass > 0.5 * (rows - 1);
+    std::vector<int> idx((size_t)rows);
+    for (int r = 0; r < rows; ++r) idx[(size_t)r] = r;
+    std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return cost[(size_t)a] > cost[(size_t)b]; });
+    for (int r = 0; r < rows; ++r) order[r] = (uint16_t)idx[(size_t)r];
+    return rows;
 }
 
 void copy_view(const LaunchParams& from, LaunchParams& to) {
@@ -441,7 +448,8 @@ void copy_view(const LaunchParams& from, LaunchParams& to) {
     to.prim_const = from.prim_const;
     std::memcpy(to.pc, from.pc, sizeof to.pc);
     std::memcpy(to.pbox, from.pbox, sizeof to.pbox);
-    to.row_rev = from.row_rev;
+    to.row_order_n = from.row_order_n;
+    std::memcpy(to.row_order, from.row_order, sizeof(uint16_t) * (size_t)from.row_order_n);
 }
 
 int view_params(rt_ctx* ctx, int W, int H, LaunchParams& lp) {
@@ -470,7 +478,7 @@ int view_params(rt_ctx* ctx, int W, int H, LaunchParams& lp) {
         }
     // RT_ROW_ORDER=0: natural row order for single-frame launches (A/B)
     const char* ro = std::getenv("RT_ROW_ORDER");
-    lp.row_rev = (ro && ro[0] == '0') ? 0 : rows_cost_low(lp, ctx->layout) ? 1 : 0;
+    lp.row_order_n = (ro && ro[0] == '0') ? 0 : row_order(lp, ctx->layout, lp.row_order);
     copy_view(lp, ctx->view_lp);
     ctx->view_cam = ctx->cam, ctx->view_w = W, ctx->view_h = H, ctx->view_ok = true;
     return RT_OK;
@@ -545,6 +553,8 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
     lp.out_fmt = fmt;
     lp.n_frames = n_frames;
     lp.out_frame_bytes = frame_bytes;
+    // the row order covers a whole frame's tile rows (band launches keep the natural order)
+    if (lp.row_order_n != (lp.local_rows + 7) / 8 || band_rows < lp.local_rows || lp.local_rows != H) lp.row_order_n = 0;
     if (enc) {
         lp.out_fmt = OUT_TILES;
         lp.enc_wire = enc->wire, lp.enc_stage = enc->stage;

@@ -122,6 +122,7 @@ struct PrimConst {
     float ocx, ocy, ocz, c;
 };
 constexpr int MAX_PRIM_CONST = 64;
+constexpr int ROW_ORDER_MAX = 272;  // tile rows of a 2176-row frame (4K UHD: 270)
 
 // Scenes with at least this many spheres use wave-bundle culling (rt_kernel.hip; the bundle
 // kernel on the 8-sphere configs measured +20 %, profiles/ab/r02_direct_converged_fold_rejected.txt).
@@ -150,9 +151,6 @@ struct LaunchParams {
     // global row = band * band_rows + r % band_rows; pixel written at out[r * W + x].
     int band_rows, band_first, band_step, local_rows;
     int n_frames;  // grid z (frames of one batch launch, all with this view); 0 = 1
-    int row_rev;   // single-frame launches: tile rows dispatched last row first (the host's cost
-                   // estimate puts the expensive rows at the bottom: they start first, the cheap ones
-                   // fill the launch's tail)
     int32_t* out;
     unsigned long long out_frame_bytes;  // batch launches: frame z of the grid at (char*)out + z * out_frame_bytes
     int out_fmt;  // 0: int32 0x00RRGGBB per pixel; 1: packed 24-bit (bytes B, G, R); 2: int32 at frame row y;
@@ -174,6 +172,11 @@ struct LaunchParams {
     int prim_const;                // 1: pc[0..S) and pbox[0..S) valid (S <= MAX_PRIM_CONST)
     PrimConst pc[MAX_PRIM_CONST];
     PrimBox pbox[MAX_PRIM_CONST];
+    // single-frame launches of a whole frame: dispatch position -> tile row, the rows in the host's
+    // estimated cost order (row_order_n = the launch's tile rows; 0: natural order).  The launch's
+    // last waves set its tail, so the expensive rows start first and the cheap ones fill the tail.
+    int row_order_n;
+    uint16_t row_order[ROW_ORDER_MAX];
 };
 
 // Debug-view segment (layout of rt_segment in include/raytracer_hip.h).

@@ -856,8 +856,8 @@ __global__ __launch_bounds__(WG_THREADS * WPG) void trace_direct_kernel(LaunchPa
     const int wave = WPG > 1 ? (int)(threadIdx.x >> 6) : 0;
     float2* lv = stk_lv + (LDS_LEVELS > 0 ? wave * LDS_LEVELS * WG_THREADS : 0);
     float* dv = stk_dv + (LDS_LEVELS > 0 ? wave * 3 * WG_THREADS : 0);
-    // single-frame launches: the host may reverse the tile-row order (LaunchParams::row_rev)
-    const int tile_y = WPG > 1 && p.row_rev ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
+    // single-frame launches: tile rows in the host's cost order (LaunchParams::row_order)
+    const int tile_y = WPG > 1 && p.row_order_n > 0 ? (int)p.row_order[blockIdx.y] : (int)blockIdx.y;
     const unsigned cnt = trace_tile_direct<K, GPOW, TILES>(p, (int)blockIdx.x * WPG + wave, tile_y, lv, dv, tl);
     add_counters<STATS>(p, threadIdx.x & 63, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
 }
