@@ -27,4 +27,3 @@ for c in C2 C3; do
             --save $O/wt_${c}_ro$ro.npz 2>&1 | grep -v amdgpu.ids | grep -v "^   (" || exit 1
     done
 done
-bash tools/r04k.sh > gpurun_out/r04k.log 2>&1 || { echo "r04k failed"; tail -20 gpurun_out/r04k.log; exit 1; }

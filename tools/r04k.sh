@@ -15,9 +15,12 @@ for v in tp1 tp2; do
 done
 for rep in 1 2; do
     for c in C2 C3; do
-        for lib in $L/libraytracer_hip.so $L/ab/libraytracer_hip_tp1.so $L/ab/libraytracer_hip_tp2.so; do
-            timeout -k 10 120 python tools/frame_wall.py --config $c --batch 1 --frames 400 --lib $lib \
-                2>&1 | grep -v amdgpu.ids | sed 's/strip=- bands=- //' || exit 1
+        for ro in 0 1; do
+            for lib in $L/libraytracer_hip.so $L/ab/libraytracer_hip_tp1.so $L/ab/libraytracer_hip_tp2.so; do
+                echo -n "[RT_ROW_ORDER=$ro] "
+                RT_ROW_ORDER=$ro timeout -k 10 120 python tools/frame_wall.py --config $c --batch 1 --frames 400 --lib $lib \
+                    2>&1 | grep -v amdgpu.ids | sed 's/strip=- bands=- //' || exit 1
+            done
         done
     done
 done

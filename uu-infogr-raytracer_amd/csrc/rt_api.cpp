@@ -402,7 +402,7 @@ PrimBox prim_box(const LaunchParams& lp, const DevSphere& s) {
 // (prim_box: shaded, with shadow rays), (1 + L)(1 + min(limit, 4)) inside a mirror sphere's box (its
 // reflected chain is shaded too).  Rows are sorted by decreasing estimate, ties in natural order.
 // The estimate only orders the workgroups: every tile is traced exactly as before.
-int row_order(const LaunchParams& lp, const SceneLayout& L, uint16_t* order) {
+int row_order(const LaunchParams& lp, const SceneLayout& L, uint16_t* order, int mode) {
     const int rows = (lp.H + 7) / 8;
     if (rows < 2 || rows > ROW_ORDER_MAX) return 0;
     const DevMaterial* mat = L.host_blob.size() >= L.off_mat + sizeof(DevMaterial) * (size_t)(L.S + L.P)
@@ -433,7 +433,19 @@ int row_order(const LaunchParams& lp, const SceneLayout& L, uint16_t* order) {
     }
     std::vector<int> idx((size_t)rows);
     for (int r = 0; r < rows; ++r) idx[(size_t)r] = r;
+    if (mode == 2) {  // (A/B) reversed
+        for (int r = 0; r < rows; ++r) order[r] = (uint16_t)(rows - 1 - r);
+        return rows;
+    }
+    if (mode == 4) {  // (A/B) natural
+        for (int r = 0; r < rows; ++r) order[r] = (uint16_t)r;
+        return rows;
+    }
     std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return cost[(size_t)a] > cost[(size_t)b]; });
+    if (mode == 3) {  // (A/B) interleaved: heaviest, lightest, second heaviest, second lightest, ...
+        for (int k = 0, lo = 0, hi = rows - 1; k < rows; ++k) order[k] = (uint16_t)idx[(size_t)(k % 2 ? hi-- : lo++)];
+        return rows;
+    }
     for (int r = 0; r < rows; ++r) order[r] = (uint16_t)idx[(size_t)r];
     return rows;
 }
@@ -449,6 +461,7 @@ void copy_view(const LaunchParams& from, LaunchParams& to) {
     std::memcpy(to.pc, from.pc, sizeof to.pc);
     std::memcpy(to.pbox, from.pbox, sizeof to.pbox);
     to.row_order_n = from.row_order_n;
+    to.col_major = from.col_major;
     std::memcpy(to.row_order, from.row_order, sizeof(uint16_t) * (size_t)from.row_order_n);
 }
 
@@ -478,7 +491,9 @@ int view_params(rt_ctx* ctx, int W, int H, LaunchParams& lp) {
         }
     // RT_ROW_ORDER=0: natural row order for single-frame launches (A/B)
     const char* ro = std::getenv("RT_ROW_ORDER");
-    lp.row_order_n = (ro && ro[0] == '0') ? 0 : row_order(lp, ctx->layout, lp.row_order);
+    lp.row_order_n = (ro && ro[0] == '0') ? 0 : row_order(lp, ctx->layout, lp.row_order, ro ? atoi(ro) : 1);
+    const char* cmj = std::getenv("RT_COL_MAJOR");
+    lp.col_major = cmj && cmj[0] == '1' ? 1 : 0;
     copy_view(lp, ctx->view_lp);
     ctx->view_cam = ctx->cam, ctx->view_w = W, ctx->view_h = H, ctx->view_ok = true;
     return RT_OK;

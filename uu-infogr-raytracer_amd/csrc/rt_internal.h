@@ -176,6 +176,7 @@ struct LaunchParams {
     // estimated cost order (row_order_n = the launch's tile rows; 0: natural order).  The launch's
     // last waves set its tail, so the expensive rows start first and the cheap ones fill the tail.
     int row_order_n;
+    int col_major;  // single-frame launches: tile rows vary fastest in dispatch order (grid x = rows)
     uint16_t row_order[ROW_ORDER_MAX];
 };
 

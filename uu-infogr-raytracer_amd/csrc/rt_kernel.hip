@@ -856,9 +856,12 @@ __global__ __launch_bounds__(WG_THREADS * WPG) void trace_direct_kernel(LaunchPa
     const int wave = WPG > 1 ? (int)(threadIdx.x >> 6) : 0;
     float2* lv = stk_lv + (LDS_LEVELS > 0 ? wave * LDS_LEVELS * WG_THREADS : 0);
     float* dv = stk_dv + (LDS_LEVELS > 0 ? wave * 3 * WG_THREADS : 0);
-    // single-frame launches: tile rows in the host's cost order (LaunchParams::row_order)
-    const int tile_y = WPG > 1 && p.row_order_n > 0 ? (int)p.row_order[blockIdx.y] : (int)blockIdx.y;
-    const unsigned cnt = trace_tile_direct<K, GPOW, TILES>(p, (int)blockIdx.x * WPG + wave, tile_y, lv, dv, tl);
+    // single-frame launches: tile rows in the host's cost order (LaunchParams::row_order), optionally
+    // with the rows varying fastest in dispatch order (col_major: grid x = tile rows)
+    const bool cm = WPG > 1 && p.col_major;
+    const int gx = cm ? (int)blockIdx.y : (int)blockIdx.x, gy = cm ? (int)blockIdx.x : (int)blockIdx.y;
+    const int tile_y = WPG > 1 && p.row_order_n > 0 ? (int)p.row_order[gy] : gy;
+    const unsigned cnt = trace_tile_direct<K, GPOW, TILES>(p, gx * WPG + wave, tile_y, lv, dv, tl);
     add_counters<STATS>(p, threadIdx.x & 63, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
 }
 
@@ -1725,7 +1728,8 @@ static void launch_variant(const LaunchParams& p, bool bundle, dim3 grid, dim3 b
     }
     else if (RT_SINGLE_WPG > 1 && !STATS && !TILES && (RT_WPG_ALL || p.n_frames <= 1) && p.copy_z == 0) {
         // a lone frame: RT_SINGLE_WPG tiles of a tile row per workgroup
-        const dim3 g((grid.x + RT_SINGLE_WPG - 1) / RT_SINGLE_WPG, grid.y, grid.z), b(WG_THREADS * RT_SINGLE_WPG);
+        const unsigned gxw = (grid.x + RT_SINGLE_WPG - 1) / RT_SINGLE_WPG;
+        const dim3 g(p.col_major ? grid.y : gxw, p.col_major ? gxw : grid.y, grid.z), b(WG_THREADS * RT_SINGLE_WPG);
         if (p.S <= DIRECT_SMAX)
             launch_by_depth<DirectK<GPOW, false, DIRECT_SMAX, false, RT_SINGLE_WPG>::template at>(p, g, b, s);
         else launch_by_depth<DirectK<GPOW, false, 0, false, RT_SINGLE_WPG>::template at>(p, g, b, s);
