@@ -42,6 +42,7 @@ internal static class Native {
     [DllImport(Lib)] internal static extern int rt_debug_segments(IntPtr ctx, int w, int h, int stride,
                                                                  [Out] Segment[] segments, int capacity, out int count);
     [DllImport(Lib)] internal static extern int rt_set_timing(IntPtr ctx, int every);
+    [DllImport(Lib)] internal static extern int rt_dispatch_order(IntPtr ctx, out int order);
 
     internal static void Check(int rc, IntPtr ctx) {
         if (rc != 0) throw new InvalidOperationException($"libraytracer_hip error {rc}: {Marshal.PtrToStringAnsi(rt_last_error(ctx))}");

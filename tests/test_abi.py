@@ -118,6 +118,7 @@ def test_null_arguments_are_errors(rtlib):
     assert rtlib.rt_create_ex(1, 0x100, C.byref(C.c_void_p())) == abi.RT_ERR_INVALID_ARG  # unknown flag
     assert rtlib.rt_count_work(None, 4, 4, None) == abi.RT_ERR_INVALID_ARG
     assert rtlib.rt_set_timing(None, 1) == abi.RT_ERR_INVALID_ARG
+    assert rtlib.rt_dispatch_order(None, C.byref(C.c_int())) == abi.RT_ERR_INVALID_ARG
     assert rtlib.rt_debug_segments(None, 4, 4, 1, None, 0, C.byref(C.c_int())) == abi.RT_ERR_INVALID_ARG
 
 

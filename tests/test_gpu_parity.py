@@ -243,6 +243,55 @@ def test_render_device_on_torch_stream(gpu_ctx, golden):
     assert crc(out.cpu().numpy()) == e["crc32"]
 
 
+@pytest.mark.parametrize("order", [0, 1, 2])
+@pytest.mark.parametrize("cid", ["C1", "C2", "C3", "REF_1280x720"])
+def test_single_frame_dispatch_orders(golden, monkeypatch, cid, order):
+    """Each single-frame dispatch order (rows by estimated cost, bottom to top, rows varying fastest:
+    rt_dispatch_order's candidates, fixed through RT_DISPATCH_ORDER) renders the golden frame, through
+    rt_render and rt_render_device."""
+    import torch
+    monkeypatch.setenv("RT_DISPATCH_ORDER", str(order))
+    e = golden["cases"][cid]
+    sc = scenes.config(e["config"]).resized(e["width"], e["height"])
+    ctx = Context(1)
+    try:
+        ctx.set_scene(sc)
+        assert ctx.dispatch_order() == order
+        assert crc(ctx.render(sc.width, sc.height)) == e["crc32"]
+        out = torch.zeros(sc.width * sc.height, dtype=torch.int32, device="cuda")
+        ctx.render_device(sc.width, sc.height, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        assert crc(out.cpu().numpy()) == e["crc32"]
+    finally:
+        ctx.close()
+
+
+def test_dispatch_order_measured_then_kept(golden):
+    """Without RT_DISPATCH_ORDER the first single-frame launches of a scene and size time the candidates
+    in turn and then keep one; every frame along the way is the golden one, and a new scene (or size)
+    measures again."""
+    import torch
+    ctx = Context(1)
+    try:
+        for cid in ("C2", "C1"):
+            e = golden["cases"][cid]
+            sc = scenes.config(e["config"]).resized(e["width"], e["height"])
+            ctx.set_scene(sc)
+            assert ctx.dispatch_order() == -1
+            outs = [torch.zeros(sc.width * sc.height, dtype=torch.int32, device="cuda") for _ in range(3)]
+            st = torch.cuda.current_stream().cuda_stream
+            for k in range(60):
+                ctx.render_device(sc.width, sc.height, outs[k % 3].data_ptr(), st)
+                if k % 10 == 9:
+                    torch.cuda.synchronize()
+            torch.cuda.synchronize()
+            assert ctx.dispatch_order() in (0, 1, 2)
+            for o in outs:
+                assert crc(o.cpu().numpy()) == e["crc32"]
+    finally:
+        ctx.close()
+
+
 def test_reference_plugin_surface_tick_and_input(oracle):
     """RayTracer(Surface).Tick()/OnKeyPress/OnMouseMove, as template.cs drives it."""
     screen = Surface(128, 96)

@@ -70,8 +70,10 @@ def main():
         res.append((time.perf_counter() - t0) / a.frames * 1e6)
     st = ctx.stats()
     kern = st["kernel_ms"] / st["launches"] * 1e3 if st["kernel_ms"] else float("nan")
+    order = ctx.dispatch_order() if hasattr(ctx, "dispatch_order") else None
     print(f"{os.path.basename(a.lib) or 'in-tree'} {a.config} {W}x{H} strip={a.strip or '-'} bands={a.bands or '-'} batch={a.batch} inflight={a.inflight}: "
-          f"wall/frame min {min(res):.2f} us median {sorted(res)[len(res)//2]:.2f} us; host enqueue/frame {min(enq):.2f} us")
+          f"wall/frame min {min(res):.2f} us median {sorted(res)[len(res)//2]:.2f} us; host enqueue/frame {min(enq):.2f} us"
+          + (f"; dispatch order {order}" if order is not None else ""))
 
 
 if __name__ == "__main__":

@@ -149,6 +149,23 @@ struct Device {
     unsigned long long* d_counters_diag = nullptr;  // rt_count_work
     std::vector<EventPair> pending, pool;
     uint64_t op_count[3] = {0, 0, 0};  // operations per timing kind (sampling phase)
+    // Dispatch order of single-frame launches (order_pick): which of the ORDER_CANDIDATES the direct
+    // kernel's workgroups follow, chosen by timing a few launches of each for the current scene and
+    // frame size.  Every order traces the same tiles the same way: only their start order differs.
+    struct OrderTuner {
+        int chosen = -1;           // -1: measuring
+        int turn = 0;              // next candidate to measure
+        int W = 0, H = 0;          // frame size and scene generation the measurements belong to
+        uint64_t scene_gen = 0, gen = 0;
+        uint64_t since = 0;        // single-frame launches since the choice (re-measured every ORDER_RETUNE)
+        std::vector<float> ms[3];
+        struct Probe {
+            hipEvent_t a = nullptr, b = nullptr;
+            int cand = 0;
+            uint64_t gen = 0;
+        };
+        std::vector<Probe> pending, pool;
+    } order;
     ncclComm_t comm = nullptr;
     int comm_rank = 0, comm_world = 0;  // rt_comm_init (one rank per process); 0 = none
 };
@@ -179,6 +196,8 @@ struct rt_ctx {
     double kernel_ms = 0, last_kernel_ms = 0, copy_ms = 0, gather_ms = 0;
     uint64_t timed[3] = {0, 0, 0};  // timed launches, copies, gathers
     int timing_every = 64;
+    uint64_t scene_gen = 0;  // rt_set_scene calls (the dispatch-order measurements belong to one scene)
+    int order_fixed = -1;    // RT_DISPATCH_ORDER=0/1/2: that candidate for every single-frame launch
     int32_t* host_staging = nullptr;
     // host ranges registered through rt_register_host and their device-mapped addresses: only
     // these are written by the trace kernels' copy slice (anything else takes hipMemcpyAsync)
@@ -402,7 +421,7 @@ PrimBox prim_box(const LaunchParams& lp, const DevSphere& s) {
 // (prim_box: shaded, with shadow rays), (1 + L)(1 + min(limit, 4)) inside a mirror sphere's box (its
 // reflected chain is shaded too).  Rows are sorted by decreasing estimate, ties in natural order.
 // The estimate only orders the workgroups: every tile is traced exactly as before.
-int row_order(const LaunchParams& lp, const SceneLayout& L, uint16_t* order, int mode) {
+int row_order(const LaunchParams& lp, const SceneLayout& L, uint16_t* order) {
     const int rows = (lp.H + 7) / 8;
     if (rows < 2 || rows > ROW_ORDER_MAX) return 0;
     const DevMaterial* mat = L.host_blob.size() >= L.off_mat + sizeof(DevMaterial) * (size_t)(L.S + L.P)
@@ -433,19 +452,7 @@ int row_order(const LaunchParams& lp, const SceneLayout& L, uint16_t* order, int
     }
     std::vector<int> idx((size_t)rows);
     for (int r = 0; r < rows; ++r) idx[(size_t)r] = r;
-    if (mode == 2) {  // (A/B) reversed
-        for (int r = 0; r < rows; ++r) order[r] = (uint16_t)(rows - 1 - r);
-        return rows;
-    }
-    if (mode == 4) {  // (A/B) natural
-        for (int r = 0; r < rows; ++r) order[r] = (uint16_t)r;
-        return rows;
-    }
     std::stable_sort(idx.begin(), idx.end(), [&](int a, int b) { return cost[(size_t)a] > cost[(size_t)b]; });
-    if (mode == 3) {  // (A/B) interleaved: heaviest, lightest, second heaviest, second lightest, ...
-        for (int k = 0, lo = 0, hi = rows - 1; k < rows; ++k) order[k] = (uint16_t)idx[(size_t)(k % 2 ? hi-- : lo++)];
-        return rows;
-    }
     for (int r = 0; r < rows; ++r) order[r] = (uint16_t)idx[(size_t)r];
     return rows;
 }
@@ -489,11 +496,7 @@ int view_params(rt_ctx* ctx, int W, int H, LaunchParams& lp) {
             lp.pc[i] = PrimConst{oc.x, oc.y, oc.z, hdot(oc, oc) - sph[i].r2};
             lp.pbox[i] = prim_box(lp, sph[i]);
         }
-    // RT_ROW_ORDER=0: natural row order for single-frame launches (A/B)
-    const char* ro = std::getenv("RT_ROW_ORDER");
-    lp.row_order_n = (ro && ro[0] == '0') ? 0 : row_order(lp, ctx->layout, lp.row_order, ro ? atoi(ro) : 1);
-    const char* cmj = std::getenv("RT_COL_MAJOR");
-    lp.col_major = cmj && cmj[0] == '1' ? 1 : 0;
+    lp.row_order_n = row_order(lp, ctx->layout, lp.row_order);  // dispatch-order candidate 0 (order_pick)
     copy_view(lp, ctx->view_lp);
     ctx->view_cam = ctx->cam, ctx->view_w = W, ctx->view_h = H, ctx->view_ok = true;
     return RT_OK;
@@ -542,6 +545,82 @@ int view_tables(rt_ctx* ctx, Device& d, LaunchParams& lp) {
     return RT_OK;
 }
 
+// Single-frame dispatch order.  A lone frame's launch ends with its slowest waves, so the order in which
+// the workgroups start sets its tail (tools/wave_times.py): cheap rows last shortens it when the costly
+// tiles are moderate (C1, C2: rows reversed or sorted by the cost estimate, -3 ... -9 %), while deep mirror
+// chains (C3: waves of 25-40 us) run faster spread over the whole launch among cheap ones (rows varying
+// fastest, -5 %) -- no one order wins every scene (profiles/ab/r04_dispatch_orders.txt).  So the library
+// measures: the first single-frame launches of a scene and frame size take the candidates in turn, each
+// bracketed by an event pair; once every candidate has ORDER_SAMPLES durations the one with the least
+// median is kept, and measured again after ORDER_RETUNE launches (the view drifts).  Candidates:
+// 0 tile rows by decreasing estimated cost (row_order), 1 tile rows bottom to top, 2 rows varying fastest
+// (column-major over the 4-tile workgroups), natural row order.
+constexpr int ORDER_CANDIDATES = 3, ORDER_SAMPLES = 5;
+constexpr uint64_t ORDER_RETUNE = 1u << 14;
+
+void order_collect(Device& d) {
+    Device::OrderTuner& t = d.order;
+    size_t keep = 0;
+    for (size_t i = 0; i < t.pending.size(); ++i) {
+        Device::OrderTuner::Probe& pr = t.pending[i];
+        if (hipEventQuery(pr.b) != hipSuccess) {
+            t.pending[keep++] = pr;
+            continue;
+        }
+        float ms = 0;
+        if (pr.gen == t.gen && hipEventElapsedTime(&ms, pr.a, pr.b) == hipSuccess)
+            t.ms[pr.cand].push_back(ms);
+        t.pool.push_back(pr);
+    }
+    t.pending.resize(keep);
+}
+
+// The candidate for this single-frame launch; *probe: bracket it with order_begin / order_end.
+int order_pick(rt_ctx* ctx, Device& d, int W, int H, bool* probe) {
+    *probe = false;
+    if (ctx->order_fixed >= 0) return ctx->order_fixed;
+    Device::OrderTuner& t = d.order;
+    if (t.W != W || t.H != H || t.scene_gen != ctx->scene_gen || (t.chosen >= 0 && ++t.since > ORDER_RETUNE)) {
+        t.W = W, t.H = H, t.scene_gen = ctx->scene_gen;
+        t.chosen = -1, t.turn = 0, t.since = 0, t.gen++;
+        for (std::vector<float>& v : t.ms) v.clear();
+    }
+    if (t.chosen >= 0) return t.chosen;
+    order_collect(d);
+    bool done = true;
+    for (const std::vector<float>& v : t.ms) done = done && v.size() >= (size_t)ORDER_SAMPLES;
+    if (done) {
+        float best = 0;
+        for (int k = 0; k < ORDER_CANDIDATES; ++k) {
+            std::vector<float> v = t.ms[k];
+            std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+            if (t.chosen < 0 || v[v.size() / 2] < best) t.chosen = k, best = v[v.size() / 2];
+        }
+        return t.chosen;
+    }
+    const int k = t.turn++ % ORDER_CANDIDATES;
+    // bound the probes in flight (results arrive as the launches complete)
+    *probe = t.ms[k].size() + t.pending.size() < (size_t)(4 * ORDER_SAMPLES * ORDER_CANDIDATES);
+    return k;
+}
+
+bool order_begin(Device& d, int cand, hipStream_t s) {
+    Device::OrderTuner& t = d.order;
+    Device::OrderTuner::Probe pr;
+    if (!t.pool.empty()) {
+        pr = t.pool.back();
+        t.pool.pop_back();
+    } else if (hipEventCreate(&pr.a) != hipSuccess || hipEventCreate(&pr.b) != hipSuccess) {
+        return false;
+    }
+    pr.cand = cand, pr.gen = t.gen;
+    (void)hipEventRecord(pr.a, s);
+    t.pending.push_back(pr);
+    return true;
+}
+
+void order_end(Device& d, hipStream_t s) { (void)hipEventRecord(d.order.pending.back().b, s); }
+
 // The fused encoder's target of a trace with out_fmt OUT_TILES (rt_render_bands_tiles).
 struct EncTarget {
     unsigned char* wire;
@@ -568,8 +647,19 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
     lp.out_fmt = fmt;
     lp.n_frames = n_frames;
     lp.out_frame_bytes = frame_bytes;
-    // the row order covers a whole frame's tile rows (band launches keep the natural order)
-    if (lp.row_order_n != (lp.local_rows + 7) / 8 || band_rows < lp.local_rows || lp.local_rows != H) lp.row_order_n = 0;
+    // single-frame launches of a whole frame on the direct kernel: the dispatch order (order_pick)
+    const bool lone = n_frames <= 1 && !enc && !(with_hand && d.hand.words) && band_rows >= lp.local_rows &&
+                      lp.local_rows == H && lp.S < CULL_MIN_SPHERES && lp.row_order_n == (H + 7) / 8;
+    bool probe = false;
+    int cand = -1;
+    if (lone) {
+        cand = order_pick(ctx, d, W, H, &probe);
+        if (cand == 1)
+            for (int r = 0; r < lp.row_order_n; ++r) lp.row_order[r] = (uint16_t)(lp.row_order_n - 1 - r);
+        if (cand == 2) lp.row_order_n = 0, lp.col_major = 1;
+    } else {
+        lp.row_order_n = 0;
+    }
     if (enc) {
         lp.out_fmt = OUT_TILES;
         lp.enc_wire = enc->wire, lp.enc_stage = enc->stage;
@@ -585,7 +675,9 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
     hipStream_t saved = d.stream;
     d.stream = stream;
     const bool timed = begin_timed(ctx, d, 0);
+    probe = probe && order_begin(d, cand, stream);
     int e = launch_trace(lp, ctx->layout.generic_pow, false, stream);
+    if (probe) order_end(d, stream);
     end_timed(d, timed);
     d.stream = saved;
     if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "trace launch failed: %s", hipGetErrorString((hipError_t)e));
@@ -668,6 +760,9 @@ int rt_create_ex(int n_gpus, int flags, rt_ctx** out_ctx) {
     if (!ctx) return fail(nullptr, RT_ERR_OOM, "out of host memory");
     ctx->n_gpus = n_gpus;
     ctx->rccl_gather = n_gpus > 1 || (flags & RT_CREATE_RCCL_GATHER) != 0;
+    // RT_DISPATCH_ORDER=0/1/2 fixes the single-frame dispatch order (order_pick; A/B and tests)
+    if (const char* o = std::getenv("RT_DISPATCH_ORDER"))
+        if (o[0] >= '0' && o[0] < '0' + ORDER_CANDIDATES && o[1] == 0) ctx->order_fixed = o[0] - '0';
     ctx->dev.resize((size_t)n_gpus);
     int cur = 0;
     (void)hipGetDevice(&cur);
@@ -724,6 +819,8 @@ void rt_destroy(rt_ctx* ctx) {
         (void)hipDeviceSynchronize();  // kernels on caller streams may still read our buffers
         for (EventPair& ep : d.pending) (void)hipEventDestroy(ep.a), (void)hipEventDestroy(ep.b);
         for (EventPair& ep : d.pool) (void)hipEventDestroy(ep.a), (void)hipEventDestroy(ep.b);
+        for (auto* v : {&d.order.pending, &d.order.pool})
+            for (Device::OrderTuner::Probe& pr : *v) (void)hipEventDestroy(pr.a), (void)hipEventDestroy(pr.b);
         if (d.comm && g_rccl.CommDestroy) (void)g_rccl.CommDestroy(d.comm);
         if (d.d_scene) (void)hipFree(d.d_scene);
         if (d.d_frame) (void)hipFree(d.d_frame);
@@ -1008,6 +1105,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
     ctx->layout = std::move(L);
     ctx->has_scene = true;
     ctx->view_ok = false;
+    ctx->scene_gen++;
     return RT_OK;
 }
 
@@ -1635,6 +1733,12 @@ int rt_get_stats(rt_ctx* ctx, rt_stats* out) {
     out->timed_launches = ctx->timed[0];
     out->timed_copies = ctx->timed[1];
     out->timed_gathers = ctx->timed[2];
+    return RT_OK;
+}
+
+int rt_dispatch_order(rt_ctx* ctx, int* out_order) {
+    if (!ctx || !out_order) return fail(ctx, RT_ERR_INVALID_ARG, "NULL argument");
+    *out_order = ctx->order_fixed >= 0 ? ctx->order_fixed : ctx->dev.empty() ? -1 : ctx->dev[0].order.chosen;
     return RT_OK;
 }
 

@@ -271,6 +271,13 @@ class Context:
         """Time every `every`-th launch/copy/gather with HIP events (0 = none; default 64)."""
         self._check(self.lib.rt_set_timing(self.ptr, int(every)))
 
+    def dispatch_order(self) -> int:
+        """The single-frame dispatch order in use (0 rows by estimated cost, 1 rows bottom to top,
+        2 rows varying fastest), -1 while the first launches still measure them (rt_dispatch_order)."""
+        o = C.c_int(-1)
+        self._check(self.lib.rt_dispatch_order(self.ptr, C.byref(o)))
+        return o.value
+
 
 class RayTracer:
     """RayTracer.cs:437-1062, public surface only, rendering on MI355X.

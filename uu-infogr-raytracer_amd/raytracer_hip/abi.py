@@ -149,6 +149,7 @@ EXPORTS = [
     ("rt_write_ppm", C.c_int, [C.c_char_p, C.c_void_p, C.c_int, C.c_int]),
     ("rt_debug_segments", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int, C.POINTER(C.c_int)]),
     ("rt_set_timing", C.c_int, [C.c_void_p, C.c_int]),
+    ("rt_dispatch_order", C.c_int, [C.c_void_p, C.POINTER(C.c_int)]),
     ("rt_get_stats", C.c_int, [C.c_void_p, C.POINTER(rt_stats)]),
     ("rt_reset_stats", C.c_int, [C.c_void_p]),
     ("rt_count_work", C.c_int, [C.c_void_p, C.c_int, C.c_int, C.POINTER(rt_work)]),
