@@ -1738,7 +1738,9 @@ int rt_get_stats(rt_ctx* ctx, rt_stats* out) {
 
 int rt_dispatch_order(rt_ctx* ctx, int* out_order) {
     if (!ctx || !out_order) return fail(ctx, RT_ERR_INVALID_ARG, "NULL argument");
-    *out_order = ctx->order_fixed >= 0 ? ctx->order_fixed : ctx->dev.empty() ? -1 : ctx->dev[0].order.chosen;
+    // (a new scene is measured again from its first single-frame launch)
+    const bool fresh = !ctx->dev.empty() && ctx->dev[0].order.scene_gen == ctx->scene_gen;
+    *out_order = ctx->order_fixed >= 0 ? ctx->order_fixed : fresh ? ctx->dev[0].order.chosen : -1;
     return RT_OK;
 }
 
