@@ -198,7 +198,6 @@ struct rt_ctx {
     int timing_every = 64;
     uint64_t scene_gen = 0;  // rt_set_scene calls (the dispatch-order measurements belong to one scene)
     int order_fixed = -1;    // RT_DISPATCH_ORDER=0/1/2: that candidate for every single-frame launch
-    int batch_order = 0;     // (A/B) RT_BATCH_ORDER
     int32_t* host_staging = nullptr;
     // host ranges registered through rt_register_host and their device-mapped addresses: only
     // these are written by the trace kernels' copy slice (anything else takes hipMemcpyAsync)
@@ -658,12 +657,6 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
         if (cand == 1)
             for (int r = 0; r < lp.row_order_n; ++r) lp.row_order[r] = (uint16_t)(lp.row_order_n - 1 - r);
         if (cand == 2) lp.row_order_n = 0, lp.col_major = 1;
-    } else if (ctx->batch_order > 0 && n_frames > 1 && !enc && band_rows >= lp.local_rows && lp.local_rows == H &&
-               lp.S < CULL_MIN_SPHERES && lp.row_order_n == (H + 7) / 8) {
-        // (A/B: RT_BATCH_ORDER=1/2/3 -- the lone-frame candidates 0/1/2 for batch launches)
-        if (ctx->batch_order == 2)
-            for (int r = 0; r < lp.row_order_n; ++r) lp.row_order[r] = (uint16_t)(lp.row_order_n - 1 - r);
-        if (ctx->batch_order == 3) lp.row_order_n = 0, lp.col_major = 1;
     } else {
         lp.row_order_n = 0;
     }
@@ -770,7 +763,6 @@ int rt_create_ex(int n_gpus, int flags, rt_ctx** out_ctx) {
     // RT_DISPATCH_ORDER=0/1/2 fixes the single-frame dispatch order (order_pick; A/B and tests)
     if (const char* o = std::getenv("RT_DISPATCH_ORDER"))
         if (o[0] >= '0' && o[0] < '0' + ORDER_CANDIDATES && o[1] == 0) ctx->order_fixed = o[0] - '0';
-    if (const char* o = std::getenv("RT_BATCH_ORDER")) ctx->batch_order = atoi(o);
     ctx->dev.resize((size_t)n_gpus);
     int cur = 0;
     (void)hipGetDevice(&cur);

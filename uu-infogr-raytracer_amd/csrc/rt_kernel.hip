@@ -858,9 +858,9 @@ __global__ __launch_bounds__(WG_THREADS * WPG) void trace_direct_kernel(LaunchPa
     float* dv = stk_dv + (LDS_LEVELS > 0 ? wave * 3 * WG_THREADS : 0);
     // single-frame launches: tile rows in the host's cost order (LaunchParams::row_order), optionally
     // with the rows varying fastest in dispatch order (col_major: grid x = tile rows)
-    const bool cm = !TILES && p.col_major;
+    const bool cm = WPG > 1 && p.col_major;
     const int gx = cm ? (int)blockIdx.y : (int)blockIdx.x, gy = cm ? (int)blockIdx.x : (int)blockIdx.y;
-    const int tile_y = !TILES && p.row_order_n > 0 ? (int)p.row_order[gy] : gy;
+    const int tile_y = WPG > 1 && p.row_order_n > 0 ? (int)p.row_order[gy] : gy;
     const unsigned cnt = trace_tile_direct<K, GPOW, TILES>(p, gx * WPG + wave, tile_y, lv, dv, tl);
     add_counters<STATS>(p, threadIdx.x & 63, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
 }
@@ -1733,12 +1733,9 @@ static void launch_variant(const LaunchParams& p, bool bundle, dim3 grid, dim3 b
         if (p.S <= DIRECT_SMAX)
             launch_by_depth<DirectK<GPOW, false, DIRECT_SMAX, false, RT_SINGLE_WPG>::template at>(p, g, b, s);
         else launch_by_depth<DirectK<GPOW, false, 0, false, RT_SINGLE_WPG>::template at>(p, g, b, s);
-    } else {
-        const dim3 g = p.col_major ? dim3(grid.y, grid.x, grid.z) : grid;  // (rows varying fastest)
-        if (p.S <= DIRECT_SMAX)
-            launch_by_depth<DirectK<GPOW, STATS, DIRECT_SMAX, TILES>::template at>(p, g, block, s);
-        else launch_by_depth<DirectK<GPOW, STATS, 0, TILES>::template at>(p, g, block, s);
-    }
+    } else if (p.S <= DIRECT_SMAX)
+        launch_by_depth<DirectK<GPOW, STATS, DIRECT_SMAX, TILES>::template at>(p, grid, block, s);
+    else launch_by_depth<DirectK<GPOW, STATS, 0, TILES>::template at>(p, grid, block, s);
 }
 
 int launch_trace(const LaunchParams& p, bool generic_pow, bool stats, void* stream) {
