@@ -27,3 +27,4 @@ for c in C2 C3; do
             2>&1 | grep -v amdgpu.ids | sed 's/strip=- bands=- //; s/; dispatch order -1//' || exit 1
     done
 done
+bash tools/r04r.sh > gpurun_out/r04r.log 2>&1 || { echo "r04r failed"; tail -20 gpurun_out/r04r.log; exit 1; }; cat gpurun_out/r04r.log
