@@ -657,9 +657,8 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
         if (cand == 1)
             for (int r = 0; r < lp.row_order_n; ++r) lp.row_order[r] = (uint16_t)(lp.row_order_n - 1 - r);
         if (cand == 2) lp.row_order_n = 0, lp.col_major = 1;
-    } else if (!(n_frames > 1 && !enc && !(with_hand && d.hand.words) && band_rows >= lp.local_rows &&
-                 lp.local_rows == H && lp.S < CULL_MIN_SPHERES && lp.row_order_n == (H + 7) / 8)) {
-        lp.row_order_n = 0;  // (whole-frame batch launches keep the estimate's order: unused by the product kernels)
+    } else {
+        lp.row_order_n = 0;
     }
     if (enc) {
         lp.out_fmt = OUT_TILES;
