@@ -26,4 +26,4 @@ for rep in 1 2; do for c in C2 C3; do for lib in lib/libraytracer_hip.so lib/ab/
     timeout -k 10 120 python tools/frame_wall.py --config $c --batch 1 --frames 400 --lib uu-infogr-raytracer_amd/$lib \
         2>&1 | grep -v amdgpu.ids | sed 's/strip=- bands=- //' || exit 1
 done; done; done
-bash tools/r04_ablate.sh || exit 1
+bash tools/rounds/r04_ablate.sh || exit 1

@@ -18,5 +18,5 @@ for cfg in C2 C4; do
     cat gpurun_out/dtrace_${cfg}_reconcile.txt
 done
 for cfg in C2 C3 C4 C5; do cat gpurun_out/trace_${cfg}_reconcile.txt; done
-bash tools/r04h.sh > gpurun_out/r04h.log 2>&1 || { tail -20 gpurun_out/r04h.log; exit 1; }
-bash tools/r04i.sh > gpurun_out/r04i.log 2>&1 || { tail -20 gpurun_out/r04i.log; exit 1; }
+bash tools/rounds/r04h.sh > gpurun_out/r04h.log 2>&1 || { tail -20 gpurun_out/r04h.log; exit 1; }
+bash tools/rounds/r04i.sh > gpurun_out/r04i.log 2>&1 || { tail -20 gpurun_out/r04i.log; exit 1; }

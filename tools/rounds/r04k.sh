@@ -1,5 +1,5 @@
 #!/bin/bash
-# r04: issue priority for long mirror chains (tools/tail_prio.patch: s_setprio 2 once a wave's lanes reach 1 / 2
+# r04: issue priority for long mirror chains (profiles/ab/r04_tail_prio.patch: s_setprio 2 once a wave's lanes reach 1 / 2
 # reflections; lib/ab/libraytracer_hip_tp1 / _tp2) against the product build: parity, single-frame wall (C2, C3),
 # and the batch shape (64-frame launches).
 set -o pipefail

@@ -1,7 +1,7 @@
 #!/bin/bash
 # r04: software-pipelined candidate loops -- the next candidate's sphere record loads while the current one is tested:
-# the merged shadow loop (tools/merged_prefetch.patch, pfm), the trace bundles' pair loop (tools/walk_prefetch.patch,
-# pfw), both (tools/prefetch_both.patch, pfb) -- against the product build: parity, then
+# the merged shadow loop (profiles/ab/r04_merged_prefetch.patch, pfm), the trace bundles' pair loop (profiles/ab/r04_walk_prefetch.patch,
+# pfw), both (profiles/ab/r04_prefetch_both.patch, pfb) -- against the product build: parity, then
 # wall per frame of 64-frame launches, C4 / C5, alternating.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}

@@ -1,5 +1,5 @@
 #!/bin/bash
-# r04: a batch launch's last frame with its tile rows in the cost estimate's order (tools/last_frame_order.patch,
+# r04: a batch launch's last frame with its tile rows in the cost estimate's order (profiles/ab/r04_last_frame_order.patch,
 # lib/ab/libraytracer_hip_lfo.so: the cheapest rows end the launch) against the product build: parity, then the
 # driver's bench shape (--steps 20 --warmup 5: one 20-frame launch) and 20-frame launches back to back, C2 / C3.
 set -o pipefail
@@ -27,4 +27,4 @@ for c in C2 C3; do
             2>&1 | grep -v amdgpu.ids | sed 's/strip=- bands=- //; s/; dispatch order -1//' || exit 1
     done
 done
-bash tools/r04r.sh > gpurun_out/r04r.log 2>&1 || { echo "r04r failed"; tail -20 gpurun_out/r04r.log; exit 1; }; cat gpurun_out/r04r.log
+bash tools/rounds/r04r.sh > gpurun_out/r04r.log 2>&1 || { echo "r04r failed"; tail -20 gpurun_out/r04r.log; exit 1; }; cat gpurun_out/r04r.log

@@ -1,5 +1,5 @@
 #!/bin/bash
-# r04: the bundle kernel at 96 SGPRs / 7 waves per SIMD (tools/sgpr96.patch: no SGPR spills in the merged
+# r04: the bundle kernel at 96 SGPRs / 7 waves per SIMD (profiles/ab/r04_sgpr96.patch: no SGPR spills in the merged
 # instantiation) against the product's 80 SGPRs / 8 waves (11 SGPRs spilled to VGPR lanes): parity, then wall per
 # frame of 64-frame launches, C4 / C5, alternating.
 set -o pipefail
