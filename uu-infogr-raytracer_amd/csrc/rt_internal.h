@@ -172,9 +172,10 @@ struct LaunchParams {
     int prim_const;                // 1: pc[0..S) and pbox[0..S) valid (S <= MAX_PRIM_CONST)
     PrimConst pc[MAX_PRIM_CONST];
     PrimBox pbox[MAX_PRIM_CONST];
-    // single-frame launches of a whole frame: dispatch position -> tile row, the rows in the host's
-    // estimated cost order (row_order_n = the launch's tile rows; 0: natural order).  The launch's
-    // last waves set its tail, so the expensive rows start first and the cheap ones fill the tail.
+    // single-frame launches of a whole frame (the direct kernel's multi-tile workgroups): dispatch
+    // position -> tile row in the order the host picked (rt_api.cpp order_pick: rows by estimated
+    // cost, or bottom to top; row_order_n = the launch's tile rows, 0: natural order).  A lone
+    // frame's last waves set its tail.
     int row_order_n;
     int col_major;  // single-frame launches: tile rows vary fastest in dispatch order (grid x = rows)
     uint16_t row_order[ROW_ORDER_MAX];
