@@ -1,6 +1,6 @@
 #!/bin/bash
 # r04: lone frames of the bundle-kernel configs (C4, C5: one frame per rt_render_device launch) -- the product
-# (natural order) and the bundle kernel with the lone-frame dispatch orders (tools/bundle_lone_order.patch,
+# (natural order) and the bundle kernel with the lone-frame dispatch orders (profiles/ab/r04_bundle_lone_order.patch,
 # lib/ab/libraytracer_hip_blo.so, RT_LONE_BUNDLE=1; measured choice and each order fixed) -- then the batch shape
 # (64-frame launches) of both builds, and the parity suite of the variant.
 set -o pipefail

@@ -198,7 +198,6 @@ struct rt_ctx {
     int timing_every = 64;
     uint64_t scene_gen = 0;  // rt_set_scene calls (the dispatch-order measurements belong to one scene)
     int order_fixed = -1;    // RT_DISPATCH_ORDER=0/1/2: that candidate for every single-frame launch
-    bool lone_bundle = false;  // (A/B, RT_LONE_BUNDLE=1: dispatch orders for the bundle kernel's lone frames)
     int32_t* host_staging = nullptr;
     // host ranges registered through rt_register_host and their device-mapped addresses: only
     // these are written by the trace kernels' copy slice (anything else takes hipMemcpyAsync)
@@ -650,8 +649,7 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
     lp.out_frame_bytes = frame_bytes;
     // single-frame launches of a whole frame on the direct kernel: the dispatch order (order_pick)
     const bool lone = n_frames <= 1 && !enc && !(with_hand && d.hand.words) && band_rows >= lp.local_rows &&
-                      lp.local_rows == H && (lp.S < CULL_MIN_SPHERES || ctx->lone_bundle) &&
-                      lp.row_order_n == (H + 7) / 8;
+                      lp.local_rows == H && lp.S < CULL_MIN_SPHERES && lp.row_order_n == (H + 7) / 8;
     bool probe = false;
     int cand = -1;
     if (lone) {
@@ -765,7 +763,6 @@ int rt_create_ex(int n_gpus, int flags, rt_ctx** out_ctx) {
     // RT_DISPATCH_ORDER=0/1/2 fixes the single-frame dispatch order (order_pick; A/B and tests)
     if (const char* o = std::getenv("RT_DISPATCH_ORDER"))
         if (o[0] >= '0' && o[0] < '0' + ORDER_CANDIDATES && o[1] == 0) ctx->order_fixed = o[0] - '0';
-    if (const char* o = std::getenv("RT_LONE_BUNDLE")) ctx->lone_bundle = o[0] == '1';
     ctx->dev.resize((size_t)n_gpus);
     int cur = 0;
     (void)hipGetDevice(&cur);
