@@ -1,6 +1,6 @@
 #!/bin/bash
 # r04: at the first fold level, the ball bound when the wave's hit points lie within K grid cells of their centre and
-# the shadow grid otherwise (tools/adapt_level1.patch, K = 1 / 2 / 4: lib/ab/libraytracer_hip_ad1/2/4) against the
+# the shadow grid otherwise (profiles/ab/r04_adapt_level1.patch, K = 1 / 2 / 4: lib/ab/libraytracer_hip_ad1/2/4) against the
 # product (grid at every level >= 1): parity, then 64-frame launches of C4 / C5, alternating.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}

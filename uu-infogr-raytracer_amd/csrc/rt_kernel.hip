@@ -1340,11 +1340,20 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
         const unsigned want = diff ? (1u << p.L) - 1u : 0u;
         // per-lane grid lookups below the first fold level, where a wave's hit points scatter; at
         // level 0 (the tile's primary hits, coherent) one bound around them culls tighter than the
-        // grid's cells (wave-uniform choice)
-        const unsigned memb = (p.shg && level >= RT_GRID_FROM_LEVEL) ? shadow_members_grid(p, hp, want)
-                                                                      : RT_FAST_MEMBERS
-                                                                            ? shadow_members_fast(p, make_shadow_sphere(hp, diff), want)
-                                                                            : shadow_members(p, make_shadow_sphere(hp, diff), want);
+        // grid's cells; at the first fold level whichever fits the wave: the ball while the hit points
+        // lie within one grid cell of their centre (light 0's cell size), the grid otherwise (C4 -1.3 %,
+        // C5 -1.6 % against the grid there, profiles/ab/r04_adaptive_level1.txt).  Wave-uniform choices.
+        unsigned memb;
+        if (p.shg && level > RT_GRID_FROM_LEVEL) {
+            memb = shadow_members_grid(p, hp, want);
+        } else if (p.shg && level == RT_GRID_FROM_LEVEL) {
+            const ShadowSphere SS = make_shadow_sphere(hp, diff);
+            const float cell = 1.0f / __builtin_fmaxf(p.shg[0].su, p.shg[0].sv);
+            memb = SS.ok && SS.R < cell ? shadow_members_fast(p, SS, want) : shadow_members_grid(p, hp, want);
+        } else {
+            memb = RT_FAST_MEMBERS ? shadow_members_fast(p, make_shadow_sphere(hp, diff), want)
+                                   : shadow_members(p, make_shadow_sphere(hp, diff), want);
+        }
         blk = shadow_merged(p, memb, hp, want, diff, act, tl);
     }
     f3 normal;
