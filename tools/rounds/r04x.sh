@@ -1,5 +1,5 @@
 #!/bin/bash
-# r04: the per-wave ball-or-grid choice at more fold levels (tools/adapt_levels.patch): aeA every level >= 1 (limit
+# r04: the per-wave ball-or-grid choice at more fold levels (profiles/ab/r04_adapt_levels.patch): aeA every level >= 1 (limit
 # 1 cell), aeB also level 0 (ball below 4 cells, the grid beyond), aeC level 0 below 16 cells -- against the product
 # (choice at level 1 only): parity, then 64-frame launches of C4 / C5, alternating.
 set -o pipefail
