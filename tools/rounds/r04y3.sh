@@ -1,6 +1,6 @@
 #!/bin/bash
 # r04: trace bundles that allow no culling take every sphere without the per-lane cull arithmetic
-# (tools/nocull.patch: ncA when the bound is unusable, ncB also when its cone is wider than 0.25) against the
+# (profiles/ab/r04_nocull.patch: ncA when the bound is unusable, ncB also when its cone is wider than 0.25) against the
 # product: parity, then 64-frame launches of C4 / C5, alternating.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-/root/repo}

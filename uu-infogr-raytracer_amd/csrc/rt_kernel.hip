@@ -1126,7 +1126,11 @@ __device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d,
     int win_s = -1;
     for (int base = 0; base < p.S; base += 64) {
         const int n = min(64, p.S - base);
-        unsigned long long m = use_box ? pmask : cull_mask(p, B, base, n);  // use_box: S <= 64
+        // use_box: S <= 64.  A bundle that allows no culling (cone of 0.5 or wider, far or non-finite
+        // origins) takes every sphere without the per-lane cull arithmetic, whose ballot would keep every
+        // sphere anyway (C4 -0.7 %, C5 -0.6 %, profiles/ab/r04_nocull_ab.txt; culling wider cones than 0.25
+        // less eagerly measured +2 %).  Wave-uniform.
+        unsigned long long m = use_box ? pmask : !B.ok ? (n == 64 ? ~0ull : (1ull << n) - 1ull) : cull_mask(p, B, base, n);
         // candidates in ascending order, selection by selects (take_*, no per-lane branches); the
         // root sequence is chosen once per wave (2a finite-positive on every lane: the usual case)
         if (__builtin_amdgcn_ballot_w64(!a2_ok) == 0)
