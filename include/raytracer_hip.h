@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 8
+#define RT_ABI_VERSION 9
 
 /* ---- status codes ---------------------------------------------------------- */
 enum {
@@ -164,15 +164,21 @@ int rt_device_count(int* out_count);
 const char* rt_last_error(const rt_ctx* ctx);
 
 /* ---- context lifetime  (replaces `new RayTracer(screen)`, RayTracer.cs:535) ---- */
-/* n_gpus >= 1.  n_gpus > 1 creates one HIP stream per device and a single-process
- * RCCL communicator (ncclCommInitAll); frames are split into interleaved row bands and
- * gathered to device 0. */
+/* n_gpus >= 1 band workers, one per device (devices 0 .. n_gpus-1; n_gpus == 1: the caller's
+ * current device), each with its own HIP stream.  A frame is split into interleaved 8-row bands,
+ * band b on worker b % n_gpus (ABI 9): rt_render / rt_render_async hand every
+ * worker's bands to the caller's host frame over that device's own PCIe link (no gather, no
+ * single-link copy of the whole frame); rt_render_device gathers them to device 0 over RCCL/xGMI
+ * (ncclCommInitAll, made on first use). */
+#define RT_MAX_WORKERS 64
 int rt_create(int n_gpus, rt_ctx** out_ctx);
-/* rt_create with flags (ABI 5).  RT_CREATE_RCCL_GATHER: rt_render takes the multi-GPU path
- * (row bands per device, ncclCommInitAll + grouped ncclGather to device 0, one-launch
- * reassembly) for any n_gpus, 1 included -- the path the C# shim uses with RT_GPUS > 1,
- * exercisable on a one-GPU machine. */
-enum { RT_CREATE_RCCL_GATHER = 1 };
+/* rt_create with flags.  RT_CREATE_RCCL_GATHER (ABI 5): rt_render gathers the bands to device 0 over
+ * RCCL (grouped ncclGather, one-launch reassembly) and copies the whole frame over device 0's link --
+ * for callers that need the frame assembled on device 0; communicators made at creation, any
+ * n_gpus, 1 included.  RT_CREATE_SHARED_DEVICE (ABI 9): all n_gpus workers on the caller's current
+ * device (a stream each) -- the multi-GPU band pipeline rehearsed on one GPU; rt_render_device then
+ * writes the workers' bands straight into the frame (no RCCL: it refuses two ranks on one device). */
+enum { RT_CREATE_RCCL_GATHER = 1, RT_CREATE_SHARED_DEVICE = 2 };
 int rt_create_ex(int n_gpus, int flags, rt_ctx** out_ctx);
 void rt_destroy(rt_ctx* ctx);
 
@@ -193,17 +199,22 @@ int rt_camera_on_mouse_move(rt_camera* camera, float delta_x, float delta_y);
 /* ---- rendering (replaces Tick(), RayTracer.cs:886-935) ---------------------- */
 /* Tick(): renders the full frame and copies it into the caller-owned host buffer
  * pixels[width*height] (Surface.pixels, 0x00RRGGBB, row-major y*width+x).
- * Synchronous: the pixels are complete on return, as template.cs:189-193 requires. */
+ * Synchronous: the pixels are complete on return, as template.cs:189-193 requires.
+ * Every worker writes its own bands into `pixels` (registered: a copy kernel through the buffer's
+ * device-mapped address, on large shares in chunks whose copies ride in the next chunk's trace
+ * launch; unregistered: the runtime's copies). */
 int rt_render(rt_ctx* ctx, int width, int height, int32_t* pixels);
 
-/* Pin a caller-owned host buffer (hipHostRegister) so rt_render's D2H copy lands
- * directly in it; the shim registers Surface.pixels once. */
+/* Pin a caller-owned host buffer (hipHostRegister, mapped into every worker's device) so that the
+ * Tick hand-off lands directly in it; the shim registers Surface.pixels once. */
 int rt_register_host(rt_ctx* ctx, void* host_ptr, size_t bytes);
 int rt_unregister_host(rt_ctx* ctx, void* host_ptr);
 
-/* Device-resident variant (single-GPU contexts): renders the frame into
- * d_pixels[width*height] on `hip_stream` (a hipStream_t; NULL = the HIP null stream, as
- * everywhere in HIP) and returns without synchronising. */
+/* Device-resident variant: renders the frame into d_pixels[width*height] (device 0's memory) on
+ * `hip_stream` (a hipStream_t of device 0; NULL = the HIP null stream, as everywhere in HIP) and
+ * returns without synchronising.  n_gpus > 1: the workers' bands are gathered to device 0 over
+ * RCCL/xGMI (RT_CREATE_SHARED_DEVICE: written straight into d_pixels), ordered after the work
+ * already on hip_stream, and hip_stream waits for the frame. */
 int rt_render_device(rt_ctx* ctx, int width, int height, int32_t* d_pixels, void* hip_stream);
 
 /* Row-band shard (one process per GPU): renders the bands b = band_first,
@@ -322,8 +333,9 @@ int rt_comm_gather(rt_ctx* ctx, const void* d_send, size_t n_bytes, void* d_recv
  * MI355X at 1080p C2 (bench.py tick_*, median of 3 x 20 frames): a display loop two frames deep
  * (rt_wait per pair) 5.2-5.3k fps, 20 frames queued 5.4-5.5k fps, against 4.9-5.0k for the
  * synchronous rt_render; a trace stream plus a copy stream ordered by events (round 2) ran
- * 1.5-5.2k fps depending on the process (profiles/r03_tick_ab.txt).  Multi-GPU contexts render
- * synchronously here (rt_render). */
+ * 1.5-5.2k fps depending on the process (profiles/r03_tick_ab.txt).  n_gpus > 1: every worker
+ * double-buffers its own band set on its own stream, and its hand-off rides in its next launch
+ * (ABI 9; RT_CREATE_RCCL_GATHER contexts render synchronously here). */
 int rt_render_async(rt_ctx* ctx, int width, int height, int32_t* pixels);
 int rt_wait(rt_ctx* ctx);
 

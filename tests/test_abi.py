@@ -57,9 +57,24 @@ def test_struct_layouts_match_header():
 
 
 def test_abi_version(rtlib):
-    assert rtlib.rt_abi_version() == 8 == abi.RT_ABI_VERSION  # 8: rt_comm_probe (7: rt_comm_* collectives)
+    # 9: the per-worker Tick hand-off, RT_CREATE_SHARED_DEVICE (8: rt_comm_probe; 7: rt_comm_* collectives)
+    assert rtlib.rt_abi_version() == 9 == abi.RT_ABI_VERSION
     hdr = open(HEADER).read()
     assert re.search(r"#define RT_ABI_VERSION (\d+)", hdr).group(1) == str(abi.RT_ABI_VERSION)
+    assert re.search(r"RT_CREATE_RCCL_GATHER = (\d+), RT_CREATE_SHARED_DEVICE = (\d+)", hdr).groups() == \
+        (str(abi.RT_CREATE_RCCL_GATHER), str(abi.RT_CREATE_SHARED_DEVICE))
+    assert re.search(r"#define RT_MAX_WORKERS (\d+)", hdr).group(1) == str(abi.RT_MAX_WORKERS)
+
+
+def test_create_flag_checks(rtlib):
+    """rt_create_ex's argument checks come before any device query (they hold on a CPU-only host): unknown
+    flags, n_gpus outside [1, RT_MAX_WORKERS], and RCCL_GATHER with SHARED_DEVICE at n > 1 (RCCL refuses two
+    ranks on one device) are argument errors."""
+    out = C.c_void_p()
+    for n, flags in [(1, 4), (0, 0), (abi.RT_MAX_WORKERS + 1, abi.RT_CREATE_SHARED_DEVICE),
+                     (2, abi.RT_CREATE_RCCL_GATHER | abi.RT_CREATE_SHARED_DEVICE)]:
+        assert rtlib.rt_create_ex(n, flags, C.byref(out)) == abi.RT_ERR_INVALID_ARG, (n, flags)
+        assert not out.value
 
 
 def test_camera_view_matches_oracle(rtlib, oracle):

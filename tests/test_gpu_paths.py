@@ -4,8 +4,7 @@
 * bench.py's timed launch shape -- balanced rt_render_bands_batch launches of up to 64 full
   1920x1080 frames, one stream (and the two-stream swap chain) -- every frame's CRC against
   tests/golden/golden.json for C2 and C3 (the north-star config);
-* the single-process RCCL gather path of rt_render (ncclCommInitAll + grouped ncclGather +
-  scatter) that the C# shim uses with RT_GPUS > 1, forced on one GPU (RT_CREATE_RCCL_GATHER);
+* (the single-process multi-GPU Tick and the forced RCCL gather path: tests/test_gpu_tick.py);
 * the headless display hand-off (rt_write_ppm) of a GPU-rendered frame vs the oracle's pixels
   (template.cs:186-209);
 * rt_count_work: nominal counts = the timed kernels' counts, executed counts bounded by them;
@@ -64,29 +63,6 @@ def test_bench_launch_shape_every_frame_golden(gpu_ctx, golden, cid, steps, infl
     st = gpu_ctx.stats()
     for k in ("primary_rays", "reflect_rays", "shadow_rays"):
         assert st[k] == steps * e["stats"][k], k  # frame 0 counts for every frame of a batch
-
-
-def test_rccl_gather_path_single_process(golden):
-    """rt_create_ex(1, RT_CREATE_RCCL_GATHER): rt_render traces 8-row bands, gathers them with
-    ncclGather (a one-rank communicator from ncclCommInitAll) and reassembles -- rt_api.cpp's
-    multi-GPU branch, on one device."""
-    e = golden["cases"]["C3"]
-    sc = scenes.config("C3")
-    with Context(1, abi.RT_CREATE_RCCL_GATHER) as ctx:
-        ctx.set_scene(sc)
-        ctx.reset_stats()
-        px = ctx.render(sc.width, sc.height).copy()
-        st = ctx.stats()
-        assert crc(px) == e["crc32"]
-        assert {k: st[k] for k in ("primary_rays", "reflect_rays", "shadow_rays")} == \
-            {k: e["stats"][k] for k in ("primary_rays", "reflect_rays", "shadow_rays")}
-        # a second frame through the same communicator (buffers reused)
-        px2 = ctx.render(sc.width, sc.height)
-        assert crc(px2) == e["crc32"]
-        ctx.set_timing(1)
-        ctx.reset_stats()
-        ctx.render(sc.width, sc.height)
-        assert ctx.stats()["timed_gathers"] == 1
 
 
 def test_ppm_of_gpu_frame_matches_oracle(tmp_path, oracle):

@@ -1,5 +1,5 @@
 """Where a lone frame's launch spends its time (tools/build_wave_times.sh builds the probe library): every
-direct-kernel wave records its start (s_memrealtime, 100 MHz), duration and HW_ID/XCC_ID.  Prints the ramp
+direct- and bundle-kernel wave records its start (s_memrealtime, 100 MHz), duration and HW_ID/XCC_ID.  Prints the ramp
 (when the waves start), the tail (when the CUs go idle), the slowest tiles and a coarse map of wave durations.
     python tools/wave_times.py --lib uu-infogr-raytracer_amd/lib/ab/libraytracer_hip_wt.so --config C2 [--batch 1]"""
 import argparse
@@ -38,7 +38,7 @@ def main():
     lib.rt_debug_wave_times.argtypes = [C.c_void_p, C.c_size_t]
     tx, ty = (W + 7) // 8, (H + 7) // 8
     n = tx * ty * a.batch
-    assert n <= 1 << 18
+    assert n <= 1 << 20
     st = torch.cuda.current_stream()
     big = torch.empty(a.batch * W * H, dtype=torch.int32, device="cuda")
 
@@ -52,7 +52,7 @@ def main():
         for _ in range(30):
             launch()
         torch.cuda.synchronize()
-        buf = np.zeros((1 << 18, 4), dtype=np.uint32)
+        buf = np.zeros((1 << 20, 4), dtype=np.uint32)
         assert lib.rt_debug_wave_times(buf.ctypes.data, buf.nbytes) == 0
         r = buf[:n]
         start = r[:, 0].astype(np.int64) | (r[:, 1].astype(np.int64) << 32)
@@ -82,9 +82,10 @@ def main():
                 f, t = divmod(int(i), tx * ty)
                 print(f"   ({t % tx:3d},{t // tx:3d},{f}) start {start[i] * TICK_US:7.2f} dur {dur[i] * TICK_US:6.2f}")
             # time series: resident waves (whole chip) per 1 us
-            edges = np.arange(0, span + 100, 100)
+            step = 100 if span < 20000 else 1000  # 1 us, or 10 us for long launches (C4/C5)
+            edges = np.arange(0, span + step, step)
             res = [(int(((start <= t) & (end > t)).sum())) for t in edges]
-            print("# resident waves per 1 us:", " ".join(str(x) for x in res))
+            print(f"# resident waves per {step // 100} us:", " ".join(str(x) for x in res))
             if a.map:
                 d = dur[: tx * ty].reshape(ty, tx).astype(float) * TICK_US
                 by, bx = max(1, ty // 34), max(1, tx // 60)

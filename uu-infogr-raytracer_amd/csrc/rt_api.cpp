@@ -2,9 +2,11 @@
 //
 // Host side of the drop-in: context lifetime, scene upload (with the scene-constant
 // precomputation described in rt_internal.h), camera math (RayTracer.cs:511-523,
-// :543-554, :892-896, :1058-1061), frame rendering (single GPU, row bands, and a
-// single-process multi-GPU path that gathers row bands over RCCL), HIP-event timing
-// and work counters.  Never throws across the ABI; no CPU fallback.
+// :543-554, :892-896, :1058-1061), frame rendering (single GPU, row bands, and the
+// single-process multi-GPU Tick: every device traces its interleaved row bands and hands
+// them to the caller's Surface.pixels over its own PCIe link; device-resident frames are
+// gathered to device 0 over RCCL/xGMI), HIP-event timing and work counters.  Never throws
+// across the ABI; no CPU fallback.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -74,9 +76,12 @@ struct Rccl {
         std::string loaded;
         dl_iterate_phdr(find_loaded_rccl, &loaded);
         if (!loaded.empty()) h = dlopen(loaded.c_str(), RTLD_NOW | RTLD_NOLOAD);
+        // RTLD_LOCAL: a RCCL loaded here must not interpose on one the process loads later (torch's own
+        // librccl, pulled in by an `import torch` after our first multi-GPU context): with RTLD_GLOBAL the
+        // two copies shared symbols and the process aborted at exit ("double free or corruption", r05b)
         const char* names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
         for (const char* n : names)
-            if (!h && (h = dlopen(n, RTLD_NOW | RTLD_GLOBAL))) break;
+            if (!h && (h = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
         if (!h) {
             err = "dlopen(librccl) failed";
             return false;
@@ -129,17 +134,16 @@ struct Device {
         int W = 0, H = 0, band_rows = 0, rank = 0, world = 0, batch_frames = 0;
         const void* wire = nullptr;
     } staged;
-    int32_t* d_frames2[2] = {nullptr, nullptr};  // rt_render_async double buffer
+    int32_t* d_frames2[2] = {nullptr, nullptr};  // rt_render_async double buffer (this device's band set)
     size_t frames2_cap[2] = {0, 0};
-    // rt_render_async: one in-order stream; frame k's D2H rides in frame k+1's launch (the copy
-    // slice, LaunchParams::copy_words) or is issued by rt_wait -- `hand` is that pending copy
+    // rt_render_async: one in-order stream per device; frame k's D2H rides in frame k+1's launch (the
+    // copy slice, LaunchParams::copy) or is issued by rt_wait -- `hand` is that pending copy
     hipStream_t async_stream = nullptr;
     struct {
-        int32_t* host = nullptr;       // caller's buffer
-        int32_t* mapped = nullptr;     // its device-mapped address (rt_register_host)
-        const int32_t* src = nullptr;  // d_frames2[slot]
-        size_t words = 0;
+        int32_t* host = nullptr;  // caller's buffer (one contiguous band set: hipMemcpyAsync on a flush)
+        CopyJob job{};            // the band set -> the buffer's device-mapped address (job.words 0: none)
     } hand;
+    hipEvent_t ev_join = nullptr;  // rt_render_device at n > 1: ordering against the caller's stream
     float* d_view_tab = nullptr;  // lx[W] then ly[H] (view_tables)
     size_t view_tab_cap = 0;
     int tab_w = -1, tab_h = -1;
@@ -184,8 +188,10 @@ struct SceneLayout {
 }  // namespace
 
 struct rt_ctx {
-    int n_gpus = 1;
-    bool rccl_gather = false;  // rt_render through row bands + RCCL gather (n_gpus > 1 or RT_CREATE_RCCL_GATHER)
+    int n_gpus = 1;            // band workers: devices, or streams on one device (RT_CREATE_SHARED_DEVICE)
+    bool rccl_gather = false;  // RT_CREATE_RCCL_GATHER: rt_render gathers the bands to device 0 over RCCL, one D2H
+    bool shared_device = false;  // RT_CREATE_SHARED_DEVICE: every worker on the caller's device
+    bool comm_all = false;       // the single-process communicators (ncclCommInitAll) exist
     std::vector<Device> dev;
     bool has_scene = false;
     SceneLayout layout;
@@ -199,12 +205,13 @@ struct rt_ctx {
     uint64_t scene_gen = 0;  // rt_set_scene calls (the dispatch-order measurements belong to one scene)
     int order_fixed = -1;    // RT_DISPATCH_ORDER=0/1/2: that candidate for every single-frame launch
     int32_t* host_staging = nullptr;
-    // host ranges registered through rt_register_host and their device-mapped addresses: only
-    // these are written by the trace kernels' copy slice (anything else takes hipMemcpyAsync)
+    // host ranges registered through rt_register_host and their device-mapped addresses (one per
+    // worker: each device writes its band set through its own mapping): only these are written by the
+    // Tick hand-off's copy kernels (anything else takes the runtime's copies)
     struct HostRange {
         char* host;
         size_t bytes;
-        char* mapped;
+        std::vector<char*> mapped;  // [worker], nullptr where the device has no mapping
     };
     std::vector<HostRange> host_ranges;
     // view_params cache: the camera and frame size of the last call (this scene) and the view part
@@ -555,7 +562,8 @@ int view_tables(rt_ctx* ctx, Device& d, LaunchParams& lp) {
 // median is kept, and measured again after ORDER_RETUNE launches (the view drifts).  Candidates:
 // 0 tile rows by decreasing estimated cost (row_order), 1 tile rows bottom to top, 2 rows varying fastest
 // (column-major over the 4-tile workgroups), natural row order.
-constexpr int ORDER_CANDIDATES = 3, ORDER_SAMPLES = 5;
+constexpr int ORDER_CANDIDATES = 3, ORDER_SAMPLES = 7;
+constexpr float ORDER_MARGIN = 1.01f;  // another order replaces candidate 0 only when > 1 % faster (median)
 constexpr uint64_t ORDER_RETUNE = 1u << 14;
 
 void order_collect(Device& d) {
@@ -590,12 +598,16 @@ int order_pick(rt_ctx* ctx, Device& d, int W, int H, bool* probe) {
     bool done = true;
     for (const std::vector<float>& v : t.ms) done = done && v.size() >= (size_t)ORDER_SAMPLES;
     if (done) {
-        float best = 0;
+        // the least median, unless candidate 0 is within the margin of it: the launches of a bench or of
+        // another process on the GPU can overlap the probes, and a noise-driven choice should not stick
+        float best = 0, med0 = 0;
         for (int k = 0; k < ORDER_CANDIDATES; ++k) {
             std::vector<float> v = t.ms[k];
             std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
+            if (k == 0) med0 = v[v.size() / 2];
             if (t.chosen < 0 || v[v.size() / 2] < best) t.chosen = k, best = v[v.size() / 2];
         }
+        if (med0 <= best * ORDER_MARGIN) t.chosen = 0;
         return t.chosen;
     }
     const int k = t.turn++ % ORDER_CANDIDATES;
@@ -628,10 +640,11 @@ struct EncTarget {
     int tiles_x, tpf, frame0;
 };
 
-// Launch the trace of bands (first, step) of `band_rows` rows into `out` on device d.
+// Launch the trace of bands (first, step) of `band_rows` rows (at most max_bands of them) into `out` on
+// device d.  `slice`: a Tick hand-off (CopyJob) that rides in the launch as its copy slice.
 int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int band_rows, int first, int step,
                 int32_t* out, int* n_bands, int fmt = RT_BANDS_INT32, int n_frames = 1, size_t frame_bytes = 0,
-                const EncTarget* enc = nullptr, bool with_hand = false) {
+                const EncTarget* enc = nullptr, const CopyJob* slice = nullptr, int max_bands = INT_MAX) {
     LaunchParams lp;
     std::memset(&lp, 0, sizeof lp);
     int rc = view_params(ctx, W, H, lp);
@@ -639,7 +652,7 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
     scene_params(ctx, d, lp);
     rc = view_tables(ctx, d, lp);
     if (rc != RT_OK) return rc;
-    const int nb = bands_of(H, band_rows, first, step);
+    const int nb = std::min(bands_of(H, band_rows, first, step), max_bands);
     if (n_bands) *n_bands = nb;
     lp.band_rows = band_rows, lp.band_first = first, lp.band_step = step;
     lp.local_rows = nb * band_rows;
@@ -648,7 +661,8 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
     lp.n_frames = n_frames;
     lp.out_frame_bytes = frame_bytes;
     // single-frame launches of a whole frame on the direct kernel: the dispatch order (order_pick)
-    const bool lone = n_frames <= 1 && !enc && !(with_hand && d.hand.words) && band_rows >= lp.local_rows &&
+    const bool with_copy = slice && slice->words;
+    const bool lone = n_frames <= 1 && !enc && !with_copy && band_rows >= lp.local_rows &&
                       lp.local_rows == H && lp.S < CULL_MIN_SPHERES && lp.row_order_n == (H + 7) / 8;
     bool probe = false;
     int cand = -1;
@@ -665,10 +679,8 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
         lp.enc_wire = enc->wire, lp.enc_stage = enc->stage;
         lp.enc_tiles_x = enc->tiles_x, lp.enc_tpf = enc->tpf, lp.enc_frame0 = enc->frame0;
     }
-    if (with_hand && d.hand.words) {  // rt_render_async: the previous frame's copy rides along
-        lp.copy_src = d.hand.src;
-        lp.copy_dst = d.hand.mapped;
-        lp.copy_words = d.hand.words;
+    if (with_copy) {  // the previous frame's (chunk's) hand-off rides along
+        lp.copy = *slice;
         lp.copy_z = 1;
         lp.out_frame_bytes = 0;
     }
@@ -681,7 +693,6 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
     end_timed(d, timed);
     d.stream = saved;
     if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "trace launch failed: %s", hipGetErrorString((hipError_t)e));
-    if (with_hand) d.hand = {};  // issued
     ctx->launches++;
     for (int k = 0; k < nb; ++k) {  // pixels of rows < H in the launched bands
         const long long y0 = (long long)(first + k * step) * band_rows;
@@ -698,28 +709,162 @@ int check_ctx(rt_ctx* ctx, int W, int H) {
     return RT_OK;
 }
 
-// Device-mapped address of [host, host + bytes) when it lies inside a range registered through
-// rt_register_host and both ends allow the copy slice's 16-byte stores; else nullptr.
-int32_t* mapped_host(const rt_ctx* ctx, void* host, size_t bytes) {
+// Worker g's device-mapped address of [host, host + bytes) when it lies inside a range registered
+// through rt_register_host and both ends allow the copy kernels' 16-byte stores; else nullptr.
+int32_t* mapped_host(const rt_ctx* ctx, int g, void* host, size_t bytes) {
     if (((uintptr_t)host & 15) != 0) return nullptr;
     const char* h = (const char*)host;
     for (const rt_ctx::HostRange& r : ctx->host_ranges)
         if (h >= r.host && bytes <= r.bytes && (size_t)(h - r.host) <= r.bytes - bytes) {
-            char* m = r.mapped + (h - r.host);
+            char* base = (size_t)g < r.mapped.size() ? r.mapped[(size_t)g] : nullptr;
+            if (!base) return nullptr;
+            char* m = base + (h - r.host);
             return ((uintptr_t)m & 15) == 0 ? (int32_t*)m : nullptr;
         }
     return nullptr;
 }
 
-// Issue rt_render_async's pending hand-off (the last frame's D2H) on the async stream.
+// The band pipeline of the Tick (the reference's only parallel loop is the row-parallel
+// one of RayTracer.cs:898-901).  Worker g of n (a device; RT_CREATE_SHARED_DEVICE: a stream of one
+// device) traces the interleaved 8-row bands b = g, g + n, ... of the frame (n == 1: the frame as one
+// band) -- balanced however the scene's cost is spread over the rows (the top ~45 % of C2 is sky) --
+// packed band after band, and hands them to the caller's frame itself.
+constexpr int TICK_BAND_ROWS = 8;
+struct Share {
+    int band_rows, first, step, nb;  // bands (first, step) of band_rows rows, nb of them
+    size_t words;                    // int32 of the packed band set inside the frame (a cut last band)
+};
+// The int32 of bands [k0, k1) of a share (the frame's last band may be cut at H).
+size_t share_words(const Share& sh, int W, int H, int k0, int k1) {
+    size_t rows = 0;
+    for (int k = k0; k < k1; ++k) {
+        const long long y0 = (long long)(sh.first + (long long)k * sh.step) * sh.band_rows;
+        rows += (size_t)std::max(0LL, std::min<long long>(sh.band_rows, (long long)H - y0));
+    }
+    return rows * (size_t)W;
+}
+Share share_of(int W, int H, int g, int n, bool banded) {
+    Share sh;
+    sh.band_rows = (n == 1 && !banded) ? H : TICK_BAND_ROWS;
+    sh.first = g, sh.step = n;
+    sh.nb = bands_of(H, sh.band_rows, g, n);
+    sh.words = share_words(sh, W, H, 0, sh.nb);
+    return sh;
+}
+// The hand-off of bands [k0, k1) of a share, traced at src (packed from band k0), into the frame whose
+// row 0 is at `frame` (a device-mapped host address or device memory of this worker).
+CopyJob share_job(const Share& sh, int W, int H, int k0, int k1, const int32_t* src, int32_t* frame) {
+    CopyJob j{};
+    const size_t bw = (size_t)sh.band_rows * (size_t)W;
+    j.src = src;
+    j.dst = frame + (size_t)(sh.first + (size_t)k0 * sh.step) * bw;
+    j.words = share_words(sh, W, H, k0, k1);
+    j.band_words = sh.step == 1 ? 0u : (unsigned)bw;  // one worker: the bands are one contiguous run
+    j.dst_stride = (unsigned long long)sh.step * bw;
+    return j;
+}
+
+// Issue each worker's pending rt_render_async hand-off (the last frame's D2H) on its async stream.
 int flush_hand(rt_ctx* ctx) {
-    if (!ctx || ctx->dev.empty()) return RT_OK;
-    Device& d = ctx->dev[0];
-    if (!d.hand.words) return RT_OK;
-    DeviceGuard guard(d.id);
-    const auto h = d.hand;
-    d.hand = {};
-    HIP_TRY(ctx, hipMemcpyAsync(h.host, h.src, h.words * sizeof(int32_t), hipMemcpyDeviceToHost, d.async_stream));
+    if (!ctx) return RT_OK;
+    for (Device& d : ctx->dev) {
+        if (!d.hand.job.words) continue;
+        DeviceGuard guard(d.id);
+        const auto h = d.hand;
+        d.hand = {};
+        if (h.host && h.job.band_words == 0) {  // one contiguous band set: the runtime's copy
+            HIP_TRY(ctx, hipMemcpyAsync(h.host, h.job.src, h.job.words * sizeof(int32_t), hipMemcpyDeviceToHost,
+                                        d.async_stream));
+        } else {
+            const int e = launch_band_copy(h.job, d.async_stream);
+            if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "hand-off copy: %s", hipGetErrorString((hipError_t)e));
+        }
+    }
+    return RT_OK;
+}
+
+// A worker's band set (src, packed) into an unregistered (or unmapped) host frame: the runtime's
+// copies, one per band (n > 1) -- the slow path; callers register Surface.pixels once.  (A pitched
+// 2-D copy into pageable memory is not used: nothing bounds what its staging writes past the last row.)
+int runtime_band_copy(rt_ctx* ctx, const Share& sh, int W, int H, const int32_t* src, int32_t* host, hipStream_t st) {
+    if (sh.nb <= 0) return RT_OK;
+    const size_t bw = (size_t)sh.band_rows * (size_t)W;
+    if (sh.step == 1) {
+        HIP_TRY(ctx, hipMemcpyAsync(host + (size_t)sh.first * bw, src, sh.words * sizeof(int32_t),
+                                    hipMemcpyDeviceToHost, st));
+        return RT_OK;
+    }
+    for (int k = 0; k < sh.nb; ++k)
+        HIP_TRY(ctx, hipMemcpyAsync(host + (size_t)(sh.first + (size_t)k * sh.step) * bw, src + (size_t)k * bw,
+                                    share_words(sh, W, H, k, k + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    return RT_OK;
+}
+
+// The single-process communicators of a multi-GPU context (ncclCommInitAll over its devices), made on
+// first use: the xGMI gather of rt_render_device at n > 1 and of RT_CREATE_RCCL_GATHER contexts.
+int ensure_comm_all(rt_ctx* ctx) {
+    if (ctx->comm_all) return RT_OK;
+    if (ctx->shared_device && ctx->n_gpus > 1)
+        return fail(ctx, RT_ERR_UNSUPPORTED, "RCCL needs one device per rank (RT_CREATE_SHARED_DEVICE context)");
+    std::string err;
+    if (!g_rccl.load(err)) return fail(ctx, RT_ERR_RCCL, "%s", err.c_str());
+    const int n = ctx->n_gpus;
+    std::vector<ncclComm_t> comms((size_t)n);
+    std::vector<int> ids((size_t)n);
+    for (int g = 0; g < n; ++g) ids[(size_t)g] = ctx->dev[(size_t)g].id;
+    const ncclResult_t r = g_rccl.CommInitAll(comms.data(), n, ids.data());
+    if (r != 0) return fail(ctx, RT_ERR_RCCL, "ncclCommInitAll: %s", g_rccl.GetErrorString ? g_rccl.GetErrorString(r) : "?");
+    for (int g = 0; g < n; ++g) ctx->dev[(size_t)g].comm = comms[(size_t)g];
+    ctx->comm_all = true;
+    return RT_OK;
+}
+
+// Every worker's bands gathered into dst (device 0, row-major frame) on device 0's stream: each device
+// traces its band set into its slot, a grouped ncclGather moves the slots to device 0 over xGMI, one
+// scatter launch per worker reassembles them there.
+int gather_frame(rt_ctx* ctx, int width, int height, int32_t* dst) {
+    int rc = ensure_comm_all(ctx);
+    if (rc != RT_OK) return rc;
+    const int n = ctx->n_gpus;
+    const int band_rows = TICK_BAND_ROWS;
+    const int max_nb = bands_of(height, band_rows, 0, n);
+    const size_t slot = (size_t)max_nb * band_rows * width;  // int32 elements per device
+    Device& d0 = ctx->dev[0];
+    for (int g = 0; g < n; ++g) {
+        Device& d = ctx->dev[(size_t)g];
+        DeviceGuard guard(d.id);
+        rc = grow(ctx, (void**)&d.d_bands, &d.bands_cap, slot * sizeof(int32_t));
+        if (rc == RT_OK && g == 0) rc = grow(ctx, (void**)&d.d_gather, &d.gather_cap, slot * n * sizeof(int32_t));
+        if (rc == RT_OK) rc = trace_bands(ctx, d, d.stream, width, height, band_rows, g, n, d.d_bands, nullptr);
+        if (rc != RT_OK) return rc;
+    }
+    std::vector<char> gtimed((size_t)n, 0);
+    for (int g = 0; g < n; ++g) {
+        DeviceGuard guard(ctx->dev[(size_t)g].id);
+        gtimed[(size_t)g] = begin_timed(ctx, ctx->dev[(size_t)g], 2);
+    }
+    if (g_rccl.GroupStart() != 0) return fail(ctx, RT_ERR_RCCL, "ncclGroupStart failed");
+    for (int g = 0; g < n; ++g) {
+        Device& d = ctx->dev[(size_t)g];
+        DeviceGuard guard(d.id);
+        const ncclResult_t r = g_rccl.Gather(d.d_bands, g == 0 ? d.d_gather : nullptr, slot, ncclInt32, 0, d.comm,
+                                             d.stream);
+        if (r != 0) {
+            (void)g_rccl.GroupEnd();
+            return fail(ctx, RT_ERR_RCCL, "ncclGather: %s", g_rccl.GetErrorString ? g_rccl.GetErrorString(r) : "?");
+        }
+    }
+    if (g_rccl.GroupEnd() != 0) return fail(ctx, RT_ERR_RCCL, "ncclGroupEnd failed");
+    for (int g = 0; g < n; ++g) {
+        DeviceGuard guard(ctx->dev[(size_t)g].id);
+        end_timed(ctx->dev[(size_t)g], gtimed[(size_t)g]);
+    }
+    DeviceGuard guard(d0.id);
+    for (int g = 0; g < n; ++g) {
+        const int nb = bands_of(height, band_rows, g, n);
+        const int e = launch_scatter_bands(d0.d_gather + slot * g, dst, width, height, band_rows, g, n, nb, d0.stream);
+        if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "scatter: %s", hipGetErrorString((hipError_t)e));
+    }
     return RT_OK;
 }
 }  // namespace
@@ -749,17 +894,22 @@ const char* rt_last_error(const rt_ctx* ctx) {
 int rt_create(int n_gpus, rt_ctx** out_ctx) { return rt_create_ex(n_gpus, 0, out_ctx); }
 
 int rt_create_ex(int n_gpus, int flags, rt_ctx** out_ctx) {
-    if (!out_ctx || n_gpus < 1 || (flags & ~RT_CREATE_RCCL_GATHER) != 0)
+    if (!out_ctx || n_gpus < 1 || n_gpus > RT_MAX_WORKERS ||
+        (flags & ~(RT_CREATE_RCCL_GATHER | RT_CREATE_SHARED_DEVICE)) != 0 ||
+        ((flags & RT_CREATE_RCCL_GATHER) && (flags & RT_CREATE_SHARED_DEVICE) && n_gpus > 1))
         return fail(nullptr, RT_ERR_INVALID_ARG, "rt_create: bad arguments");
     *out_ctx = nullptr;
+    const bool shared = (flags & RT_CREATE_SHARED_DEVICE) != 0;
     int ndev = 0;
     if (rt_device_count(&ndev) != RT_OK || ndev == 0)
         return fail(nullptr, RT_ERR_NO_DEVICE, "no HIP device visible (libraytracer_hip has no CPU fallback)");
-    if (n_gpus > ndev) return fail(nullptr, RT_ERR_NO_DEVICE, "rt_create(%d): only %d devices visible", n_gpus, ndev);
+    if (n_gpus > ndev && !shared)
+        return fail(nullptr, RT_ERR_NO_DEVICE, "rt_create(%d): only %d devices visible", n_gpus, ndev);
     rt_ctx* ctx = new (std::nothrow) rt_ctx();
     if (!ctx) return fail(nullptr, RT_ERR_OOM, "out of host memory");
     ctx->n_gpus = n_gpus;
-    ctx->rccl_gather = n_gpus > 1 || (flags & RT_CREATE_RCCL_GATHER) != 0;
+    ctx->rccl_gather = (flags & RT_CREATE_RCCL_GATHER) != 0;
+    ctx->shared_device = shared;
     // RT_DISPATCH_ORDER=0/1/2 fixes the single-frame dispatch order (order_pick; A/B and tests)
     if (const char* o = std::getenv("RT_DISPATCH_ORDER"))
         if (o[0] >= '0' && o[0] < '0' + ORDER_CANDIDATES && o[1] == 0) ctx->order_fixed = o[0] - '0';
@@ -768,7 +918,7 @@ int rt_create_ex(int n_gpus, int flags, rt_ctx** out_ctx) {
     (void)hipGetDevice(&cur);
     for (int g = 0; g < n_gpus; ++g) {
         Device& d = ctx->dev[(size_t)g];
-        d.id = n_gpus == 1 ? cur : g;  // one device: the caller's current one
+        d.id = (n_gpus == 1 || shared) ? cur : g;  // one device: the caller's current one
         DeviceGuard guard(d.id);
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, d.id) == hipSuccess && std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
@@ -788,24 +938,13 @@ int rt_create_ex(int n_gpus, int flags, rt_ctx** out_ctx) {
             return rc;
         }
     }
-    if (ctx->rccl_gather) {
-        std::string err;
-        if (!g_rccl.load(err)) {
-            fail(ctx, RT_ERR_RCCL, "%s", err.c_str());
-            rt_destroy(ctx);
-            return RT_ERR_RCCL;
-        }
-        std::vector<ncclComm_t> comms((size_t)n_gpus);
-        std::vector<int> ids((size_t)n_gpus);
-        for (int g = 0; g < n_gpus; ++g) ids[(size_t)g] = ctx->dev[(size_t)g].id;
-        ncclResult_t r = g_rccl.CommInitAll(comms.data(), n_gpus, ids.data());
-        if (r != 0) {
-            fail(ctx, RT_ERR_RCCL, "ncclCommInitAll: %s", g_rccl.GetErrorString ? g_rccl.GetErrorString(r) : "?");
+    if (ctx->rccl_gather) {  // the gather's communicators now, so that a missing RCCL fails here
+        const int rc = ensure_comm_all(ctx);
+        if (rc != RT_OK) {
             g_last_error = ctx->last_error;
             rt_destroy(ctx);
-            return RT_ERR_RCCL;
+            return rc;
         }
-        for (int g = 0; g < n_gpus; ++g) ctx->dev[(size_t)g].comm = comms[(size_t)g];
     }
     *out_ctx = ctx;
     return RT_OK;
@@ -821,6 +960,7 @@ void rt_destroy(rt_ctx* ctx) {
         for (EventPair& ep : d.pool) (void)hipEventDestroy(ep.a), (void)hipEventDestroy(ep.b);
         for (auto* v : {&d.order.pending, &d.order.pool})
             for (Device::OrderTuner::Probe& pr : *v) (void)hipEventDestroy(pr.a), (void)hipEventDestroy(pr.b);
+        if (d.ev_join) (void)hipEventDestroy(d.ev_join);
         if (d.comm && g_rccl.CommDestroy) (void)g_rccl.CommDestroy(d.comm);
         if (d.d_scene) (void)hipFree(d.d_scene);
         if (d.d_frame) (void)hipFree(d.d_frame);
@@ -1181,11 +1321,41 @@ int rt_render_device(rt_ctx* ctx, int width, int height, int32_t* d_pixels, void
     int rc = check_ctx(ctx, width, height);
     if (rc != RT_OK) return rc;
     if (!d_pixels) return fail(ctx, RT_ERR_INVALID_ARG, "NULL d_pixels");
-    if (ctx->n_gpus != 1) return fail(ctx, RT_ERR_INVALID_ARG, "rt_render_device needs a single-GPU context");
-    Device& d = ctx->dev[0];
-    DeviceGuard guard(d.id);
+    Device& d0 = ctx->dev[0];
     hipStream_t s = (hipStream_t)hip_stream;  // NULL = the HIP null stream
-    rc = trace_bands(ctx, d, s, width, height, height, 0, 1, d_pixels, nullptr);
+    if (ctx->n_gpus == 1 && !ctx->rccl_gather) {
+        DeviceGuard guard(d0.id);
+        rc = trace_bands(ctx, d0, s, width, height, height, 0, 1, d_pixels, nullptr);
+    } else {
+        // n > 1: the workers start after the work already on the caller's stream (d_pixels may be in use)
+        // and the caller's stream waits for the whole frame
+        for (Device& d : ctx->dev)
+            if (!d.ev_join) {
+                DeviceGuard guard(d.id);
+                HIP_TRY(ctx, hipEventCreateWithFlags(&d.ev_join, hipEventDisableTiming));
+            }
+        {
+            DeviceGuard guard(d0.id);
+            HIP_TRY(ctx, hipEventRecord(d0.ev_join, s));
+        }
+        for (Device& d : ctx->dev) {
+            DeviceGuard guard(d.id);
+            HIP_TRY(ctx, hipStreamWaitEvent(d.stream, d0.ev_join, 0));
+        }
+        if (ctx->shared_device) {  // one device: every worker writes its bands straight into the frame
+            for (int g = 0; g < ctx->n_gpus && rc == RT_OK; ++g)
+                rc = trace_bands(ctx, ctx->dev[(size_t)g], ctx->dev[(size_t)g].stream, width, height, TICK_BAND_ROWS,
+                                 g, ctx->n_gpus, d_pixels, nullptr, RT_BANDS_FRAME);
+        } else {  // the RCCL gather to device 0 over xGMI, reassembled into d_pixels on device 0's stream
+            rc = gather_frame(ctx, width, height, d_pixels);
+        }
+        if (rc != RT_OK) return rc;
+        DeviceGuard guard(d0.id);
+        for (size_t g = 0; g < (ctx->shared_device ? ctx->dev.size() : 1); ++g) {
+            HIP_TRY(ctx, hipEventRecord(ctx->dev[g].ev_join, ctx->dev[g].stream));
+            HIP_TRY(ctx, hipStreamWaitEvent(s, ctx->dev[g].ev_join, 0));
+        }
+    }
     if (rc == RT_OK) {
         ctx->frames++;
         ctx->pixels += (uint64_t)width * (uint64_t)height;
@@ -1488,13 +1658,22 @@ int rt_comm_gather(rt_ctx* ctx, const void* d_send, size_t n_bytes, void* d_recv
 int rt_register_host(rt_ctx* ctx, void* host_ptr, size_t bytes) {
     if (!ctx || !host_ptr || !bytes) return fail(ctx, RT_ERR_INVALID_ARG, "rt_register_host: bad arguments");
     DeviceGuard guard(ctx->dev[0].id);
-    HIP_TRY(ctx, hipHostRegister(host_ptr, bytes, hipHostRegisterDefault));
-    // the device-mapped address lets rt_render_async's trace launches write the frame into it
-    void* mapped = nullptr;
-    if (hipHostGetDevicePointer(&mapped, host_ptr, 0) == hipSuccess && mapped)
-        ctx->host_ranges.push_back({(char*)host_ptr, bytes, (char*)mapped});
-    else
-        (void)hipGetLastError();  // not mapped: rt_render_async copies with hipMemcpyAsync
+    // mapped into every device's address space: each worker's copy kernel writes its own bands
+    hipError_t e = hipHostRegister(host_ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        HIP_TRY(ctx, hipHostRegister(host_ptr, bytes, hipHostRegisterDefault));
+    }
+    rt_ctx::HostRange r{(char*)host_ptr, bytes, std::vector<char*>(ctx->dev.size(), nullptr)};
+    for (size_t g = 0; g < ctx->dev.size(); ++g) {
+        DeviceGuard dg(ctx->dev[g].id);
+        void* mapped = nullptr;
+        if (hipHostGetDevicePointer(&mapped, host_ptr, 0) == hipSuccess && mapped)
+            r.mapped[g] = (char*)mapped;
+        else
+            (void)hipGetLastError();  // not mapped on this device: its hand-off takes the runtime's copies
+    }
+    ctx->host_ranges.push_back(std::move(r));
     return RT_OK;
 }
 
@@ -1513,89 +1692,109 @@ int rt_unregister_host(rt_ctx* ctx, void* host_ptr) {
     return RT_OK;
 }
 
+namespace {
+// Chunks of a worker's share in a synchronous Tick: its bands are traced in `chunks` launches and the
+// copy of chunk c rides in the launch of chunk c + 1 (the last one by the copy kernel alone), so the
+// PCIe-bound copy runs under the trace instead of after it.  RT_TICK_CHUNKS=1..8 fixes the count;
+// by default it grows with the share (a chunk of ~4 M pixels or more: a 1080p frame is one chunk).
+int tick_chunks(const rt_ctx* ctx, int W, int H) {
+    if (const char* e = std::getenv("RT_TICK_CHUNKS")) {
+        const int k = std::atoi(e);
+        if (k >= 1 && k <= 8) return k;
+    }
+    const double share = (double)W * H / ctx->n_gpus;
+    return share >= 16e6 ? 4 : share >= 4e6 ? 2 : 1;
+}
+
+// The synchronous Tick of every worker: each traces its band set and copies it into `pixels` on its
+// own stream (its own device and PCIe link); the host waits for all of them at the end.
+int tick_sync(rt_ctx* ctx, int W, int H, int32_t* pixels) {
+    const int n = ctx->n_gpus;
+    const size_t frame_bytes = (size_t)W * H * sizeof(int32_t);
+    const int chunks = tick_chunks(ctx, W, H);
+    for (int g = 0; g < n; ++g) {
+        Device& d = ctx->dev[(size_t)g];
+        DeviceGuard guard(d.id);
+        int32_t* mapped = mapped_host(ctx, g, pixels, frame_bytes);
+        const int nc = mapped ? chunks : 1;
+        const Share sh = share_of(W, H, g, n, nc > 1);
+        if (sh.nb <= 0) continue;
+        int rc = grow(ctx, (void**)&d.d_bands, &d.bands_cap, (size_t)sh.nb * sh.band_rows * W * sizeof(int32_t));
+        if (rc != RT_OK) return rc;
+        if (!mapped || (n == 1 && nc == 1)) {  // unregistered, or the whole frame on one device: runtime's copy
+            rc = trace_bands(ctx, d, d.stream, W, H, sh.band_rows, sh.first, sh.step, d.d_bands, nullptr);
+            if (rc != RT_OK) return rc;
+            const bool ctimed = begin_timed(ctx, d, 1);
+            rc = runtime_band_copy(ctx, sh, W, H, d.d_bands, pixels, d.stream);
+            end_timed(d, ctimed);
+            if (rc != RT_OK) return rc;
+            continue;
+        }
+        CopyJob prev{};
+        for (int c = 0; c < nc; ++c) {
+            const int k0 = (int)((long long)sh.nb * c / nc), k1 = (int)((long long)sh.nb * (c + 1) / nc);
+            if (k1 <= k0) continue;
+            int32_t* out = d.d_bands + (size_t)k0 * sh.band_rows * W;
+            rc = trace_bands(ctx, d, d.stream, W, H, sh.band_rows, sh.first + k0 * sh.step, sh.step, out, nullptr,
+                             RT_BANDS_INT32, 1, 0, nullptr, &prev, k1 - k0);
+            if (rc != RT_OK) return rc;
+            prev = share_job(sh, W, H, k0, k1, out, mapped);
+        }
+        const bool ctimed = begin_timed(ctx, d, 1);
+        const int e = launch_band_copy(prev, d.stream);
+        end_timed(d, ctimed);
+        if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "hand-off copy: %s", hipGetErrorString((hipError_t)e));
+    }
+    for (Device& d : ctx->dev) {
+        DeviceGuard guard(d.id);
+        HIP_TRY(ctx, hipStreamSynchronize(d.stream));
+    }
+    return RT_OK;
+}
+}  // namespace
+
 // Tick(): full frame into the caller's Surface.pixels, synchronous.
 int rt_render(rt_ctx* ctx, int width, int height, int32_t* pixels) {
     int rc = check_ctx(ctx, width, height);
     if (rc != RT_OK) return rc;
     if (!pixels) return fail(ctx, RT_ERR_INVALID_ARG, "NULL pixels");
-    const size_t frame_bytes = (size_t)width * height * sizeof(int32_t);
-    Device& d0 = ctx->dev[0];
-    if (d0.hand.words) {  // rt_render_async frames first (the caller may reuse their buffers)
-        rc = rt_wait(ctx);
+    for (const Device& d : ctx->dev)
+        if (d.hand.job.words) {  // rt_render_async frames first (the caller may reuse their buffers)
+            rc = rt_wait(ctx);
+            if (rc != RT_OK) return rc;
+            break;
+        }
+    if (ctx->rccl_gather) {  // bands gathered to device 0 over RCCL, then the whole frame over its link
+        Device& d0 = ctx->dev[0];
+        const size_t frame_bytes = (size_t)width * height * sizeof(int32_t);
+        {
+            DeviceGuard guard(d0.id);
+            rc = grow(ctx, (void**)&d0.d_frame, &d0.frame_cap, frame_bytes);
+            if (rc != RT_OK) return rc;
+        }
+        rc = gather_frame(ctx, width, height, d0.d_frame);
         if (rc != RT_OK) return rc;
-    }
-    if (!ctx->rccl_gather) {
         DeviceGuard guard(d0.id);
-        rc = grow(ctx, (void**)&d0.d_frame, &d0.frame_cap, frame_bytes);
-        if (rc != RT_OK) return rc;
-        rc = trace_bands(ctx, d0, d0.stream, width, height, height, 0, 1, d0.d_frame, nullptr);
-        if (rc != RT_OK) return rc;
+        const bool ctimed = begin_timed(ctx, d0, 1);
+        HIP_TRY(ctx, hipMemcpyAsync(pixels, d0.d_frame, frame_bytes, hipMemcpyDeviceToHost, d0.stream));
+        end_timed(d0, ctimed);
+        HIP_TRY(ctx, hipStreamSynchronize(d0.stream));
     } else {
-        // interleaved row bands: band b -> device b % n; each device traces its
-        // band set into a padded slot; RCCL gathers the slots to device 0 over xGMI, where
-        // they are scattered back into the row-major frame.
-        const int n = ctx->n_gpus;
-        const int band_rows = 8;
-        const int max_nb = bands_of(height, band_rows, 0, n);
-        const size_t slot = (size_t)max_nb * band_rows * width;  // int32 elements per device
-        for (int g = 0; g < n; ++g) {
-            Device& d = ctx->dev[(size_t)g];
-            DeviceGuard guard(d.id);
-            rc = grow(ctx, (void**)&d.d_bands, &d.bands_cap, slot * sizeof(int32_t));
-            if (rc != RT_OK) return rc;
-            if (g == 0) {
-                rc = grow(ctx, (void**)&d.d_gather, &d.gather_cap, slot * n * sizeof(int32_t));
-                if (rc == RT_OK) rc = grow(ctx, (void**)&d.d_frame, &d.frame_cap, frame_bytes);
-                if (rc != RT_OK) return rc;
-            }
-            rc = trace_bands(ctx, d, d.stream, width, height, band_rows, g, n, d.d_bands, nullptr);
-            if (rc != RT_OK) return rc;
-        }
-        std::vector<char> gtimed((size_t)n, 0);
-        for (int g = 0; g < n; ++g) {
-            DeviceGuard guard(ctx->dev[(size_t)g].id);
-            gtimed[g] = begin_timed(ctx, ctx->dev[(size_t)g], 2);
-        }
-        if (g_rccl.GroupStart() != 0) return fail(ctx, RT_ERR_RCCL, "ncclGroupStart failed");
-        for (int g = 0; g < n; ++g) {
-            Device& d = ctx->dev[(size_t)g];
-            DeviceGuard guard(d.id);
-            ncclResult_t r = g_rccl.Gather(d.d_bands, g == 0 ? d.d_gather : nullptr, slot, ncclInt32, 0, d.comm,
-                                           d.stream);
-            if (r != 0) {
-                (void)g_rccl.GroupEnd();
-                return fail(ctx, RT_ERR_RCCL, "ncclGather: %s", g_rccl.GetErrorString ? g_rccl.GetErrorString(r) : "?");
-            }
-        }
-        if (g_rccl.GroupEnd() != 0) return fail(ctx, RT_ERR_RCCL, "ncclGroupEnd failed");
-        for (int g = 0; g < n; ++g) {
-            DeviceGuard guard(ctx->dev[(size_t)g].id);
-            end_timed(ctx->dev[(size_t)g], gtimed[g]);
-        }
-        DeviceGuard guard(d0.id);
-        for (int g = 0; g < n; ++g) {
-            const int nb = bands_of(height, band_rows, g, n);
-            int e = launch_scatter_bands(d0.d_gather + slot * g, d0.d_frame, width, height, band_rows, g, n, nb,
-                                         d0.stream);
-            if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "scatter: %s", hipGetErrorString((hipError_t)e));
-        }
+        rc = tick_sync(ctx, width, height, pixels);
+        if (rc != RT_OK) return rc;
     }
-    DeviceGuard guard(d0.id);
-    const bool ctimed = begin_timed(ctx, d0, 1);
-    HIP_TRY(ctx, hipMemcpyAsync(pixels, d0.d_frame, frame_bytes, hipMemcpyDeviceToHost, d0.stream));
-    end_timed(d0, ctimed);
-    HIP_TRY(ctx, hipStreamSynchronize(d0.stream));
     ctx->frames++;
     ctx->pixels += (uint64_t)width * (uint64_t)height;
     return RT_OK;
 }
 
-// Double-buffered Tick() on one in-order stream.  Frame k is traced into device buffer k % 2;
-// its D2H copy rides in frame k+1's launch as the copy slice (grid z = 0, dispatched ahead of the
-// trace workgroups, so the PCIe-bound copy of frame k runs under the trace of frame k+1) or is
-// issued by rt_wait.  Buffer k % 2 is traced again by launch k+2, after launch k+1 (its copy) on the
-// same stream.  The slice writes only host ranges registered through rt_register_host (their
-// device-mapped addresses); any other buffer gets hipMemcpyAsync on the same stream.
+// Double-buffered Tick() on one in-order stream per worker.  Frame k's band set is traced into device
+// buffer k % 2; its D2H copy rides in frame k+1's launch as the copy slice (grid z = 0, dispatched
+// ahead of the trace workgroups, so the PCIe-bound copy of frame k runs under the trace of frame k+1)
+// or is issued by rt_wait.  Buffer k % 2 is traced again by launch k+2, after launch k+1 (its copy) on
+// the same stream.  The slice writes only host ranges registered through rt_register_host (their
+// device-mapped addresses); any other buffer gets the runtime's copies on the same stream.  n > 1: every
+// worker does the same with its own bands, stream and PCIe link.
 // Measured (profiles/r03_tick_ab.txt): a trace stream and a copy stream ordered by events ran
 // 175-195 us per frame in some processes and 350-1200 us in others -- torch's own kernel-on-one-
 // stream / D2H-on-another pattern does the same -- while one stream ran a steady 195-200 us with
@@ -1605,31 +1804,37 @@ int rt_render_async(rt_ctx* ctx, int width, int height, int32_t* pixels) {
     if (rc != RT_OK) return rc;
     if (!pixels) return fail(ctx, RT_ERR_INVALID_ARG, "NULL pixels");
     if (ctx->rccl_gather) return rt_render(ctx, width, height, pixels);
-    Device& d = ctx->dev[0];
-    DeviceGuard guard(d.id);
     const size_t frame_bytes = (size_t)width * height * sizeof(int32_t);
-    if (!d.async_stream) HIP_TRY(ctx, hipStreamCreateWithFlags(&d.async_stream, hipStreamNonBlocking));
-    const int slot = d.async_next;
-    if (d.frames2_cap[slot] < frame_bytes) {  // (re)allocation: the pending copy may read the other
-        rc = flush_hand(ctx);                 // buffer only, but nothing may still use this one
+    const int n = ctx->n_gpus;
+    for (int g = 0; g < n; ++g) {
+        Device& d = ctx->dev[(size_t)g];
+        DeviceGuard guard(d.id);
+        if (!d.async_stream) HIP_TRY(ctx, hipStreamCreateWithFlags(&d.async_stream, hipStreamNonBlocking));
+        const int slot = d.async_next;
+        const Share sh = share_of(width, height, g, n, false);
+        const size_t bytes = std::max<size_t>(1, (size_t)sh.nb * sh.band_rows * width) * sizeof(int32_t);
+        if (d.frames2_cap[slot] < bytes || sh.nb <= 0) {  // (re)allocation: the pending copy may read the
+            rc = flush_hand(ctx);                         // other buffer only, but nothing may still use
+            if (rc != RT_OK) return rc;                   // this one
+            HIP_TRY(ctx, hipStreamSynchronize(d.async_stream));
+        }
+        if (sh.nb <= 0) continue;  // (more workers than bands)
+        rc = grow(ctx, (void**)&d.d_frames2[slot], &d.frames2_cap[slot], bytes);
         if (rc != RT_OK) return rc;
-        HIP_TRY(ctx, hipStreamSynchronize(d.async_stream));
+        rc = trace_bands(ctx, d, d.async_stream, width, height, sh.band_rows, sh.first, sh.step, d.d_frames2[slot],
+                         nullptr, RT_BANDS_INT32, 1, 0, nullptr, d.hand.job.words ? &d.hand.job : nullptr);
+        if (rc != RT_OK) return rc;
+        d.hand = {};  // issued (in the launch)
+        int32_t* mapped = mapped_host(ctx, g, pixels, frame_bytes);
+        if (mapped) {
+            d.hand.host = sh.step == 1 ? pixels : nullptr;
+            d.hand.job = share_job(sh, width, height, 0, sh.nb, d.d_frames2[slot], mapped);
+        } else {
+            rc = runtime_band_copy(ctx, sh, width, height, d.d_frames2[slot], pixels, d.async_stream);
+            if (rc != RT_OK) return rc;
+        }
+        d.async_next = slot ^ 1;
     }
-    rc = grow(ctx, (void**)&d.d_frames2[slot], &d.frames2_cap[slot], frame_bytes);
-    if (rc != RT_OK) return rc;
-    rc = trace_bands(ctx, d, d.async_stream, width, height, height, 0, 1, d.d_frames2[slot], nullptr, RT_BANDS_INT32,
-                     1, 0, nullptr, true);
-    if (rc != RT_OK) return rc;
-    int32_t* mapped = mapped_host(ctx, pixels, frame_bytes);
-    if (mapped) {
-        d.hand.host = pixels;
-        d.hand.mapped = mapped;
-        d.hand.src = d.d_frames2[slot];
-        d.hand.words = (size_t)width * height;
-    } else {
-        HIP_TRY(ctx, hipMemcpyAsync(pixels, d.d_frames2[slot], frame_bytes, hipMemcpyDeviceToHost, d.async_stream));
-    }
-    d.async_next = slot ^ 1;
     ctx->frames++;
     ctx->pixels += (uint64_t)width * (uint64_t)height;
     return RT_OK;
@@ -1738,8 +1943,10 @@ int rt_get_stats(rt_ctx* ctx, rt_stats* out) {
 
 int rt_dispatch_order(rt_ctx* ctx, int* out_order) {
     if (!ctx || !out_order) return fail(ctx, RT_ERR_INVALID_ARG, "NULL argument");
-    // (a new scene is measured again from its first single-frame launch)
-    const bool fresh = !ctx->dev.empty() && ctx->dev[0].order.scene_gen == ctx->scene_gen;
+    // (a new scene or frame size is measured again from its first single-frame launch)
+    if (ctx->dev.empty()) return fail(ctx, RT_ERR_INVALID_ARG, "context without a device");
+    const Device::OrderTuner& t = ctx->dev[0].order;
+    const bool fresh = t.scene_gen == ctx->scene_gen && ctx->view_ok && t.W == ctx->view_w && t.H == ctx->view_h;
     *out_order = ctx->order_fixed >= 0 ? ctx->order_fixed : fresh ? ctx->dev[0].order.chosen : -1;
     return RT_OK;
 }

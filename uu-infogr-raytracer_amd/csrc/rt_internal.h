@@ -129,6 +129,19 @@ constexpr int ROW_ORDER_MAX = 272;  // tile rows of a 2176-row frame (4K UHD: 27
 constexpr int CULL_MIN_SPHERES = 12;
 
 
+// A band set's copy into a frame (the Tick hand-off, rt_api.cpp share_of): `words` int32 of a packed
+// band set at src -> dst, band after band: source word i of band k = i / band_words lands at dst word
+// k * dst_stride + i % band_words (band_words = 0: one contiguous run).  The host guarantees 16-byte
+// aligned ends and band_words, dst_stride multiples of 4 (whole 16-byte stores never straddle a band).
+struct CopyJob {
+    const int32_t* src;
+    int32_t* dst;
+    unsigned long long words;
+    unsigned long long dst_stride;
+    unsigned band_words;
+    unsigned pad;
+};
+
 // Per-launch parameters (passed by value as the kernel argument block, < 4 KiB).
 struct LaunchParams {
     const DevSphere* sph;
@@ -161,13 +174,11 @@ struct LaunchParams {
     uint32_t* enc_stage;
     int enc_tiles_x, enc_tpf, enc_frame0;
     unsigned long long* counters;  // COUNTER_SLOTS x COUNTER_STRIDE (CNT_*)
-    // rt_render_async's fused hand-off: with copy_z = 1 the launch has one more grid z-slice,
-    // z = 0, whose workgroups copy copy_words int32 from copy_src (the previous frame, device) to
-    // copy_dst (its caller's registered host buffer, device-mapped address); the launch's one
-    // frame is z = 1 (out_frame_bytes 0).  copy_z = 0: no slice.
-    const int32_t* copy_src;
-    int32_t* copy_dst;
-    unsigned long long copy_words;
+    // The Tick hand-off fused into a trace launch (rt_render_async: the previous frame; a chunked
+    // rt_render: the previous chunk): with copy_z = 1 the launch has one more grid z-slice, z = 0,
+    // whose workgroups run `copy` (device band set -> the caller's registered host buffer through its
+    // device-mapped address); the launch's one frame is z = 1 (out_frame_bytes 0).  copy_z = 0: none.
+    CopyJob copy;
     int copy_z;
     int prim_const;                // 1: pc[0..S) and pbox[0..S) valid (S <= MAX_PRIM_CONST)
     PrimConst pc[MAX_PRIM_CONST];
@@ -180,6 +191,8 @@ struct LaunchParams {
     int col_major;  // single-frame launches: tile rows vary fastest in dispatch order (grid x = rows)
     uint16_t row_order[ROW_ORDER_MAX];
 };
+// The kernel argument block: raising ROW_ORDER_MAX or MAX_PRIM_CONST must not push it past 4 KiB.
+static_assert(sizeof(LaunchParams) < 4096, "LaunchParams is passed by value as the kernarg block (< 4 KiB)");
 
 // Debug-view segment (layout of rt_segment in include/raytracer_hip.h).
 struct DevSegment {
@@ -198,6 +211,9 @@ int launch_scatter_gathered(const unsigned char* g, size_t slot_bytes, int fmt, 
                             int band_rows, int world, void* stream);
 int launch_scatter_bands(const int32_t* bands, int32_t* frame, int W, int H, int band_rows, int band_first,
                          int band_step, int n_bands, void* stream);
+// A CopyJob on its own (the Tick hand-off when no later trace launch carries it: the last chunk of a
+// synchronous rt_render, rt_wait's flush of rt_render_async's last frame).
+int launch_band_copy(const CopyJob& job, void* stream);
 
 constexpr int OUT_TILES = 3;
 

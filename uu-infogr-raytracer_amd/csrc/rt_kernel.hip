@@ -210,34 +210,55 @@ __device__ __forceinline__ uint32_t shift_channel(float c) {
 // row y (format 2), or packed 24-bit (B, G, R bytes; the top byte of the int32 is always 0)
 // for band sets shipped to rank 0 -- a quarter fewer bytes over xGMI (format 1).
 // Format 2 (RT_BANDS_FRAME): the rank's bands straight into the row-major frame (row y).
-// The copy slice (z = 0) of rt_render_async's launch: the previous frame, device -> the caller's
-// registered host buffer, 16 bytes per lane (both ends 16-byte aligned, checked on the host).
-// Dispatched before the trace workgroups of the same launch, so the PCIe-bound copy of frame k-1
-// runs under the trace of frame k on one in-order stream.  Only the slice's first COPY_WAVES
-// workgroups copy (grid-strided, 4 loads in flight per lane), the others exit at once: a wave
-// holds its slot until its host stores are acknowledged, and a slice of one-store waves (8,100 at
-// 1080p) held nearly every wave slot of the chip until PCIe had drained them, so the trace waited.
+// The Tick hand-off (CopyJob): a band set, device -> the caller's registered host buffer through its
+// device-mapped address, 16 bytes per lane (both ends 16-byte aligned, checked on the host), band k
+// of the packed source at k * dst_stride in the frame (one band set per device of a multi-GPU Tick,
+// each device's bands cross its own PCIe link).  As a trace launch's copy slice (z = 0)
+// it is dispatched before the trace workgroups, so the PCIe-bound copy of frame (or chunk) k-1 runs
+// under the trace of k on one in-order stream.  Only the first COPY_WAVES workgroups copy
+// (grid-strided, 4 loads in flight per lane), the others exit at once: a wave holds its slot until its
+// host stores are acknowledged, and a slice of one-store waves (8,100 at 1080p) held nearly every wave
+// slot of the chip until PCIe had drained them, so the trace waited.
 constexpr unsigned COPY_WAVES = 512;
-__device__ __forceinline__ void copy_slice(const LaunchParams& p) {
+__device__ __forceinline__ size_t band_dst(const CopyJob& j, unsigned i) {  // source word -> frame word
+    if (j.band_words == 0) return i;
+    const unsigned k = i / j.band_words;  // (words < 2^31: W * H is capped on the host)
+    return (size_t)k * j.dst_stride + (i - k * j.band_words);
+}
+__device__ __forceinline__ void copy_job(const CopyJob& j, size_t wg, size_t nwg) {
     const size_t lane = threadIdx.x & 63;
-    const size_t nwg = min((size_t)gridDim.x * gridDim.y, (size_t)COPY_WAVES);
-    const size_t wg = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
-    if (wg >= nwg) return;
-    const unsigned long long n = p.copy_words, n4 = n / 4;
-    const int4* __restrict__ s4 = (const int4*)p.copy_src;
-    int4* __restrict__ d4 = (int4*)p.copy_dst;
+    const unsigned long long n = j.words, n4 = n / 4;
+    const int4* __restrict__ s4 = (const int4*)j.src;
     const size_t step = nwg * 64;
     size_t i = wg * 64 + lane;
-    for (; i + 3 * step < n4; i += 4 * step) {
-        const int4 a = s4[i], b = s4[i + step], c = s4[i + 2 * step], d = s4[i + 3 * step];
-        d4[i] = a;
-        d4[i + step] = b;
-        d4[i + 2 * step] = c;
-        d4[i + 3 * step] = d;
+    if (j.band_words == 0) {
+        int4* __restrict__ d4 = (int4*)j.dst;
+        for (; i + 3 * step < n4; i += 4 * step) {
+            const int4 a = s4[i], b = s4[i + step], c = s4[i + 2 * step], d = s4[i + 3 * step];
+            d4[i] = a;
+            d4[i + step] = b;
+            d4[i + 2 * step] = c;
+            d4[i + 3 * step] = d;
+        }
+        for (; i < n4; i += step) d4[i] = s4[i];
+    } else {  // band_words and dst_stride are multiples of 4: a 16-byte chunk never straddles a band
+        // (one chunk per lane and iteration, 32-bit chunk indices: this path shares the trace kernels'
+        // register allocation, which must not grow -- 512 waves keep ~0.5 MB in flight, plenty for PCIe)
+        int4* __restrict__ d4 = (int4*)j.dst;
+        const unsigned bq = j.band_words / 4, sq = (unsigned)(j.dst_stride / 4);
+        for (unsigned c = (unsigned)i; c < (unsigned)n4; c += (unsigned)step) {
+            const unsigned k = c / bq;
+            d4[k * sq + (c - k * bq)] = s4[c];
+        }
     }
-    for (; i < n4; i += step) d4[i] = s4[i];
-    if (wg == 0 && lane < n - n4 * 4) p.copy_dst[n4 * 4 + lane] = p.copy_src[n4 * 4 + lane];
+    if (wg == 0 && lane < n - n4 * 4) j.dst[band_dst(j, (unsigned)(n4 * 4 + lane))] = j.src[n4 * 4 + lane];
 }
+__device__ __forceinline__ void copy_slice(const LaunchParams& p) {
+    const size_t nwg = min((size_t)gridDim.x * gridDim.y, (size_t)COPY_WAVES);
+    const size_t wg = (size_t)blockIdx.y * gridDim.x + blockIdx.x;
+    if (wg < nwg) copy_job(p.copy, wg, nwg);
+}
+__global__ __launch_bounds__(64) void band_copy_kernel(CopyJob j) { copy_job(j, blockIdx.x, gridDim.x); }
 
 __device__ __forceinline__ void store_pixel(const LaunchParams& p, int r, int y, int x, uint32_t px32) {
     const size_t i = (size_t)(p.out_fmt == 2 ? y : r) * (size_t)p.W + (size_t)x;
@@ -839,7 +860,7 @@ __device__ __forceinline__ unsigned trace_tile_direct(const LaunchParams& p, int
 // STATS: the diagnostic build that also tallies the work actually executed (not timed).
 // TILES: out_fmt OUT_TILES (the fused encoder: its own instantiation, so that the others keep their
 // register budget -- the epilogue alone raises the direct kernel's SGPR peak from 79 to 83).
-// WPG: waves (8x8 tiles of a tile row) per workgroup -- 1 for batch launches; RT_SINGLE_WPG for
+// WPG: waves (8x8 tiles of a tile row) per workgroup -- 1 for batch launches; SINGLE_WPG for
 // single-frame launches without a copy slice (fewer, larger workgroups: the dispatcher launches
 // one-wave groups no faster than ~6.9 us per 1080p frame, a floor a lone frame's launch pays in
 // full, tools/launch_probe.hip).  Each wave has its own LDS stack slice.
@@ -860,7 +881,7 @@ __global__ __launch_bounds__(WG_THREADS * WPG) void trace_direct_kernel(LaunchPa
     // with the rows varying fastest in dispatch order (col_major: grid x = tile rows)
     const bool cm = WPG > 1 && p.col_major;
     const int gx = cm ? (int)blockIdx.y : (int)blockIdx.x, gy = cm ? (int)blockIdx.x : (int)blockIdx.y;
-    const int tile_y = WPG > 1 && p.row_order_n > 0 ? (int)p.row_order[gy] : gy;
+    const int tile_y = WPG > 1 && gy < p.row_order_n ? (int)p.row_order[gy] : gy;
     const unsigned cnt = trace_tile_direct<K, GPOW, TILES>(p, gx * WPG + wave, tile_y, lv, dv, tl);
     add_counters<STATS>(p, threadIdx.x & 63, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
 }
@@ -1169,16 +1190,14 @@ __device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d,
 // for light li (lights some lane wants only).  Converged call.  (Hoisting the light-independent
 // terms of the cull out of the light loop cut VALU 1.8 % but spilled 12 B/lane: C4 +0.8 %, C5 +0.8 %,
 // profiles/ab/r03_shadow_queue_rejected.txt.)
-// shadow_members with the light-independent terms hoisted out of the light loop (the merged
-// instantiation, whose register budget has room for them; RT_FAST_MEMBERS): lane i loads sphere
+// Candidate sets of the lights from the level's ball bound, with the light-independent terms hoisted
+// out of the light loop (the merged instantiation, whose register budget has room for them; against
+// one shadow_sphere_cull per light: C4 -2.6 %, profiles/ab/r04_fast_members_ab.txt): lane i loads sphere
 // i's centre and r' once, w = C - O, the world-frame L1 bound dc >= |C - O| and the threshold T of
 // the line rule once, and per light only projects w onto (U, V, A) -- FMA allowed, culling only --
 // and applies the same two rules: line miss if |w_perp|^2 > T^2, behind if w.A < -(R + mgn).  The
 // margins are shadow_sphere_cull's: 2^-8 (dc + 3R) with dc from the unprojected w, plus 2^-18
 // (|O| + |C|_1) for the rounding of w and of its projections (each < 2^-21 |w|_1, far inside).
-#ifndef RT_FAST_MEMBERS
-#define RT_FAST_MEMBERS 1
-#endif
 __device__ __forceinline__ unsigned shadow_members_fast(const LaunchParams& p, const ShadowSphere& SS, unsigned want) {
     const int lane = threadIdx.x & 63;
     const bool in = lane < p.S;
@@ -1207,16 +1226,6 @@ __device__ __forceinline__ unsigned shadow_members_fast(const LaunchParams& p, c
     }
     return memb;
 }
-__device__ __forceinline__ unsigned shadow_members(const LaunchParams& p, const ShadowSphere& SS, unsigned want) {
-    const int lane = threadIdx.x & 63;
-    unsigned memb = 0;
-    for (int li = 0; li < p.L; ++li)
-        if (__builtin_amdgcn_ballot_w64((want >> li) & 1u) != 0) {
-            const unsigned long long cm = shadow_sphere_cull(p, SS, p.li[li], li, 0, p.S);
-            memb |= ((cm >> lane) & 1ull) ? (1u << li) : 0u;
-        }
-    return memb;
-}
 // OR of a 32-bit value over the wave (all 64 lanes active): DPP row rotations give each 16-lane row
 // its OR, four readlanes finish it.
 __device__ __forceinline__ unsigned wave_or(unsigned v) {
@@ -1228,9 +1237,9 @@ __device__ __forceinline__ unsigned wave_or(unsigned v) {
            (unsigned)__builtin_amdgcn_readlane((int)v, 32) | (unsigned)__builtin_amdgcn_readlane((int)v, 48);
 }
 
-#ifndef RT_GRID_FROM_LEVEL
-#define RT_GRID_FROM_LEVEL 1
-#endif
+// The fold level from which the shadow grids serve (below it the ball bound; at it, per wave, whichever
+// fits: shade_bundle).  Level 2 measured C4 +0.6 %, C5 -1.3 % (profiles/ab/r04_w2all_and_grid_level2.txt).
+constexpr int GRID_FROM_LEVEL = 1;
 // Candidate sets of the lights from the per-light shadow grids (p.shg != nullptr; rt_internal.h
 // DevShadowGrid, host tables and the exactness argument in rt_api.cpp build_shadow_grid): each
 // lane wanting light li looks up the grid cell of its own hit point's (u, v) and the axial slab of
@@ -1348,15 +1357,14 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
         // lie within one grid cell of their centre (light 0's cell size), the grid otherwise (C4 -1.3 %,
         // C5 -1.6 % against the grid there, profiles/ab/r04_adaptive_level1.txt).  Wave-uniform choices.
         unsigned memb;
-        if (p.shg && level > RT_GRID_FROM_LEVEL) {
+        if (p.shg && level > GRID_FROM_LEVEL) {
             memb = shadow_members_grid(p, hp, want);
-        } else if (p.shg && level == RT_GRID_FROM_LEVEL) {
+        } else if (p.shg && level == GRID_FROM_LEVEL) {
             const ShadowSphere SS = make_shadow_sphere(hp, diff);
             const float cell = 1.0f / __builtin_fmaxf(p.shg[0].su, p.shg[0].sv);
             memb = SS.ok && SS.R < cell ? shadow_members_fast(p, SS, want) : shadow_members_grid(p, hp, want);
         } else {
-            memb = RT_FAST_MEMBERS ? shadow_members_fast(p, make_shadow_sphere(hp, diff), want)
-                                   : shadow_members(p, make_shadow_sphere(hp, diff), want);
+            memb = shadow_members_fast(p, make_shadow_sphere(hp, diff), want);
         }
         blk = shadow_merged(p, memb, hp, want, diff, act, tl);
     }
@@ -1712,12 +1720,8 @@ struct DirectK {
         static constexpr auto fn = trace_direct_kernel<K, GPOW, STATS, SMAX, TILES, WPG>;
     };
 };
-#ifndef RT_SINGLE_WPG
-#define RT_SINGLE_WPG 4
-#endif
-#ifndef RT_WPG_ALL
-#define RT_WPG_ALL 0
-#endif
+// tiles of a tile row per workgroup for single-frame launches (8: +2.5 % on C2, profiles/r04_final_check.txt)
+constexpr int SINGLE_WPG = 4;
 template <bool GPOW, bool STATS, bool TILES, bool MERGED>
 struct BundleK {
     template <int K>
@@ -1739,13 +1743,13 @@ static void launch_variant(const LaunchParams& p, bool bundle, dim3 grid, dim3 b
         else
             launch_by_depth<BundleK<GPOW, STATS, TILES, false>::template at>(p, grid, block, s);
     }
-    else if (RT_SINGLE_WPG > 1 && !STATS && !TILES && (RT_WPG_ALL || p.n_frames <= 1) && p.copy_z == 0) {
-        // a lone frame: RT_SINGLE_WPG tiles of a tile row per workgroup
-        const unsigned gxw = (grid.x + RT_SINGLE_WPG - 1) / RT_SINGLE_WPG;
-        const dim3 g(p.col_major ? grid.y : gxw, p.col_major ? gxw : grid.y, grid.z), b(WG_THREADS * RT_SINGLE_WPG);
+    else if (SINGLE_WPG > 1 && !STATS && !TILES && p.n_frames <= 1 && p.copy_z == 0) {
+        // a lone frame: SINGLE_WPG tiles of a tile row per workgroup
+        const unsigned gxw = (grid.x + SINGLE_WPG - 1) / SINGLE_WPG;
+        const dim3 g(p.col_major ? grid.y : gxw, p.col_major ? gxw : grid.y, grid.z), b(WG_THREADS * SINGLE_WPG);
         if (p.S <= DIRECT_SMAX)
-            launch_by_depth<DirectK<GPOW, false, DIRECT_SMAX, false, RT_SINGLE_WPG>::template at>(p, g, b, s);
-        else launch_by_depth<DirectK<GPOW, false, 0, false, RT_SINGLE_WPG>::template at>(p, g, b, s);
+            launch_by_depth<DirectK<GPOW, false, DIRECT_SMAX, false, SINGLE_WPG>::template at>(p, g, b, s);
+        else launch_by_depth<DirectK<GPOW, false, 0, false, SINGLE_WPG>::template at>(p, g, b, s);
     } else if (p.S <= DIRECT_SMAX)
         launch_by_depth<DirectK<GPOW, STATS, DIRECT_SMAX, TILES>::template at>(p, grid, block, s);
     else launch_by_depth<DirectK<GPOW, STATS, 0, TILES>::template at>(p, grid, block, s);
@@ -1790,6 +1794,14 @@ int launch_scatter_gathered(const unsigned char* g, size_t slot_bytes, int fmt, 
     if (blocks > 8192) blocks = 8192;
     hipLaunchKernelGGL(scatter_gathered_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, g,
                        slot_bytes, fmt, frame, W, H, band_rows, world);
+    return (int)hipGetLastError();
+}
+
+int launch_band_copy(const CopyJob& job, void* stream) {
+    if (job.words == 0) return (int)hipSuccess;
+    const unsigned long long chunks = (job.words + 3) / 4;
+    const unsigned wg = (unsigned)min((unsigned long long)COPY_WAVES, (chunks + 63) / 64);
+    hipLaunchKernelGGL(band_copy_kernel, dim3(wg), dim3(64), 0, (hipStream_t)stream, job);
     return (int)hipGetLastError();
 }
 

@@ -77,8 +77,9 @@ class Context:
     """Thin owner of an rt_ctx*."""
 
     def __init__(self, n_gpus: int = 1, flags: int = 0):
-        """flags: abi.RT_CREATE_RCCL_GATHER routes rt_render through the multi-GPU band +
-        RCCL-gather path even on one device (rt_create_ex)."""
+        """n_gpus band workers, one per device (rt_create_ex).  flags: abi.RT_CREATE_RCCL_GATHER routes
+        rt_render through the RCCL gather to device 0 (even on one device); abi.RT_CREATE_SHARED_DEVICE
+        puts every worker on the current device (the multi-GPU Tick rehearsed on one GPU)."""
         self.lib = load_library()
         self.ptr = C.c_void_p()
         check(self.lib, self.lib.rt_create_ex(int(n_gpus), int(flags), C.byref(self.ptr)))

@@ -14,9 +14,11 @@ PKG_ROOT = os.path.dirname(_HERE)
 # RAYTRACER_HIP_LIB selects another build of the library (A/B variants under lib/ab/)
 LIB_PATH = os.environ.get("RAYTRACER_HIP_LIB") or os.path.join(PKG_ROOT, "lib", "libraytracer_hip.so")
 
-RT_ABI_VERSION = 8  # include/raytracer_hip.h
+RT_ABI_VERSION = 9  # include/raytracer_hip.h
 RT_COMM_ID_BYTES = 128
 RT_CREATE_RCCL_GATHER = 1
+RT_CREATE_SHARED_DEVICE = 2
+RT_MAX_WORKERS = 64
 RT_BANDS_INT32, RT_BANDS_RGB24, RT_BANDS_FRAME = 0, 1, 2
 RT_OK = 0
 RT_ERR_INVALID_ARG = -1
