@@ -2,20 +2,23 @@
 """bench.py -- the hot path of BASELINE.json on MI355X.
 
 One step = one frame of the per-pixel trace (RayTracer.Tick, Raytracer/RayTracer.cs:886-935)
-on the configuration named by --config (default C2 = BASELINE.json configs[1]: 1920x1080,
-8 spheres + 1 plane, 1 light, depth 1), with the scene resident in HBM and the frame written
-to HBM.
+on the configuration named by --config (default C3 = BASELINE.json configs[2], the north-star's
+target config: 1920x1080, 8 spheres + 1 plane, 2 lights, recursive mirror reflections depth 4),
+with the scene resident in HBM and the frame written to HBM.
 
 N = 1: the timed frames run as balanced launches of up to 64 frames (rt_render_bands_batch),
 one launch in flight, back to back on one stream: HIP events around the timed region / launches
 give roofline.kernel_avg_ms (which rocprofv3's kernel trace of the same command reproduces); an
-untimed second pass times each launch with its own event pair (kernel_avg_ms_launch_events).  C3 (the north-star config:
-depth 4, 2 lights) is measured in the same run ("also").
+untimed second pass times each launch with its own event pair (kernel_avg_ms_launch_events).  C2 (configs[1]: depth 1,
+1 light), C4 and C5 are measured in the same run ("also"), and the plugin path's Tick() (rt_render / rt_render_async
+into registered host memory, PCIe included) for C2-C5 under tick_by_config.
 
 N > 1 (`--gpus N`: one process per GPU; started here through torch.distributed.run when no
 launcher set WORLD_SIZE): the frame is split into interleaved 8-row bands, band b on rank
 b % N, and the band sets are gathered to rank 0 over RCCL (torch.distributed backend "nccl"
-is RCCL on ROCm) -- strong scaling of a fixed frame.
+is RCCL on ROCm) -- strong scaling of a fixed frame.  Then rank 0 runs the plugin path's own multi-GPU
+Tick() in one process (Context(N): every device hands its bands to the host frame over its own PCIe
+link), reported under plugin_tick.
 
 Prints ONE JSON line (rank 0).  Rays = primary + reflected + shadow rays of the visible
 (nearest-hit) path, counted by the kernel itself (rt_get_stats); `work_per_frame` sets the
@@ -51,16 +54,22 @@ def parse(argv=None):
     ap.add_argument("--min-warmup-ms", type=float, default=50.0,
                     help="N=1: keep warming up (untimed, whole launches) until this much wall time has passed -- "
                          "the GPU needs ~10-50 ms of load to reach its steady clock; reported as warmup_effective")
-    ap.add_argument("--config", default="C2")
+    ap.add_argument("--config", default="C3",
+                    help="the bench line's config (default C3: BASELINE configs[2], the north-star's 1080p depth-4 "
+                         "target; C2 = configs[1] runs under 'also')")
     ap.add_argument("--also-dist", default="C5",
                     help="N>1: comma list of further configs run through the same band pipeline after --config and "
                          "reported under 'also' (default C5: 7680x4320, the config BASELINE names for the 1/2/4/8-GPU "
                          "scaling curve); '' = none")
-    ap.add_argument("--also", default="C3,C4,C5",
+    ap.add_argument("--also", default="C2,C4,C5",
                     help="N=1: comma list of further configs measured in the same run and reported under 'also' "
-                         "(default C3, the north-star config: depth 4, 2 lights; C4, 3840x2160 with 64 spheres, "
+                         "(default C2, BASELINE configs[1]: depth 1, 1 light; C4, 3840x2160 with 64 spheres, "
                          "4 lights, depth 6 -- BASELINE's LDS/compaction stress config; and C5, the 7680x4320 "
                          "config of BASELINE's 1/2/4/8-GPU curve -- the N > 1 lines carry it as also.C5); '' = none")
+    ap.add_argument("--tick-configs", default="C2,C4,C5",
+                    help="configs whose plugin-path Tick() rates (rt_render / rt_render_async into registered host "
+                         "memory, PCIe included) are reported under tick_by_config beside the bench config's own "
+                         "(N > 1: rank 0's single-process Context(N) leg, plugin_tick); '' = none")
     ap.add_argument("--size", default="",
                     help="WxH: probe runs only -- the config's scene at another frame size (never the bench line)")
     ap.add_argument("--band-rows", type=int, default=8)
@@ -435,6 +444,50 @@ def tick_rates(ctx, W, H, torch, n=20, reps=3, n_single=200):
     return out
 
 
+def plugin_ticks(ctx, configs, scenes, n=20, reps=3):
+    """The plugin path's Tick() per config (RayTracer.Tick -> rt_render / rt_render_async into registered
+    host buffers, the frame complete in host memory -- PCIe included; never `value`), median of `reps` runs
+    of n frames: tick_fps (synchronous), tick_async_fps (two frames deep, a wait per pair) and the frame
+    bytes per second they move to the host (d2h_gbs).  ctx: a Context of any worker count (its devices
+    each hand their own bands over their own link)."""
+    import numpy as np
+    out = {}
+    for name in configs:
+        sc = scenes.config(name)
+        W, H = sc.width, sc.height
+        ctx.set_scene(sc)
+        bufs = [np.zeros(W * H, dtype=np.int32) for _ in range(2)]
+        for b in bufs:
+            ctx.register_host(b)
+
+        def sync():
+            for _ in range(n):
+                ctx.render(W, H, bufs[0])
+
+        def pair():
+            for k in range(n):
+                ctx.render_async(W, H, bufs[k % 2])
+                if k % 2:
+                    ctx.wait()
+            ctx.wait()
+        e = {}
+        for key, fn in (("tick_fps", sync), ("tick_async_fps", pair)):
+            fn()  # warm
+            rates = []
+            for _ in range(reps):
+                t = time.perf_counter()
+                fn()
+                rates.append(n / (time.perf_counter() - t))
+            e[key] = sorted(rates)[len(rates) // 2]
+            e[key + "_runs"] = [round(r, 1) for r in rates]
+            e[key.replace("fps", "d2h_gbs")] = W * H * 4 * e[key] / 1e9
+        e["frame_mb"] = W * H * 4 / 1e6
+        for b in bufs:
+            ctx.unregister_host(b)
+        out[sc.name] = e
+    return out
+
+
 def main():
     args = parse()
     action, msg = world_check(args)
@@ -488,6 +541,26 @@ def main():
             out.setdefault("also", {})[o2["config"]["workload"].split(":")[0]] = {
                 k: o2[k] for k in ("value", "unit", "n_gpus", "steps", "ms_per_step", "fps", "config", "roofline",
                                    "verified_frames") if k in o2}
+    tick_cfgs = [c for c in (x.strip() for x in args.tick_configs.split(",")) if c]
+    if not args.no_tick and (tick_cfgs or args.config) and world > 1:
+        # The plugin path's own multi-GPU Tick() (what RayTracer.Tick with RT_GPUS = N runs): ONE process,
+        # Context(N) -- every device traces its interleaved bands and hands them to the host frame over its
+        # own PCIe link.  Rank 0 drives all N devices; the other ranks wait at the barrier.  (The rehearsal
+        # on fewer GPUs: the N workers share the device, RT_CREATE_SHARED_DEVICE.)
+        dist.barrier()
+        if rank == 0:
+            try:
+                flags = abi.RT_CREATE_SHARED_DEVICE if args.rehearse_gloo else 0
+                with Context(world, flags) as pctx:
+                    pt = plugin_ticks(pctx, [args.config] + [c for c in tick_cfgs if c != args.config], scenes)
+                pt["n_workers"] = world
+                pt["note"] = (f"single process, Context({world}){' shared-device rehearsal' if flags else ''}: "
+                              f"rt_render (synchronous) / rt_render_async (two frames deep) into registered host "
+                              f"buffers, every device's bands over its own PCIe link; median of 3 runs of 20 frames")
+            except Exception as e:  # reported, never fatal for the line
+                pt = {"error": repr(e)}
+            out["plugin_tick"] = pt
+        dist.barrier()
     if rank == 0:
         print(json.dumps(out), flush=True)
     dist.destroy_process_group()
@@ -1051,6 +1124,17 @@ def main_single(args, torch, Context, abi, scenes):
                                           "vs *_run = exact tests / shadow rays the kernel executed (skipped: shadow "
                                           "tests that cannot change the pixel, culled spheres)")
         out.update(tick_rates(ctx, W, H, torch))
+        # the single-frame dispatch order the library measured and kept for this scene (rt_dispatch_order;
+        # RT_DISPATCH_ORDER fixes it): single_launch_fps depends on it
+        out["dispatch_order"] = ctx.dispatch_order()
+        tick_cfgs = [c for c in (x.strip() for x in args.tick_configs.split(",")) if c]
+        if tick_cfgs:
+            out["tick_by_config"] = plugin_ticks(ctx, tick_cfgs, scenes)
+            out["tick_by_config"]["note"] = ("plugin-path Tick() per config, one GPU: tick_fps = rt_render (synchronous, "
+                                             "large frames in chunks whose PCIe copy rides in the next chunk's trace), "
+                                             "tick_async_fps = rt_render_async two frames deep; d2h_gbs = frame bytes "
+                                             "x fps; median of 3 runs of 20 frames")
+            ctx.set_scene(sc)
     also = [c for c in (x.strip() for x in args.also.split(",")) if c and c.upper() != sc.name.upper()]
     if also:
         out["also"] = {}
@@ -1069,13 +1153,14 @@ def main_single(args, torch, Context, abi, scenes):
                 out["also"][sc2.name]["valu_frac"] = (per_frame * 64 / (r2["kernel_ms_per_frame"] / 1e3) / 1e12
                                                       / VALU_PEAK_TOPS)
     if not args.no_cpu_baseline:
-        # the bench config, then C3 (the north-star config: 1080p with reflections), C1
-        # (BASELINE configs[0]) and the verbatim reference scene beside it
-        c3 = scenes.config("C3")
-        c3_rays = out.get("also", {}).get("C3", {}).get("rays_per_frame")
+        # the bench config, then the other 1080p config (C2 beside C3: BASELINE.md's "C2/C3 at 1920x1080
+        # beside the GPU"), C1 (BASELINE configs[0]) and the verbatim reference scene beside it
+        other = "C2" if sc.name.upper() == "C3" else "C3"
+        o_sc = scenes.config(other)
+        o_rays = out.get("also", {}).get(other, {}).get("rays_per_frame")
         cpu_samples = [(sc, r["rays_per_frame"], 0.4)]
-        if sc.name.upper() != "C3":
-            cpu_samples.append((c3, c3_rays, 0.25))
+        if sc.name.upper() != other:
+            cpu_samples.append((o_sc, o_rays, 0.25))
         cpu_samples += [(scenes.config("C1"), None, 0.15), (scenes.reference(512, 512), None, 0.2)]
         out["cpu_baseline"] = cpu_baseline(cpu_samples, args.cpu_seconds)
     print(json.dumps(out), flush=True)

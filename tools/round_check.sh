@@ -1,19 +1,38 @@
 #!/bin/bash
-# GPU box, end of a change: smoke, the whole GPU suite, the bench line of every config, the
-# one-process rehearsal of the N>1 path.  Each step under its own limit; stops at a crash.
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out
-step() {
-    local name=$1 limit=$2; shift 2
-    timeout -k 10 "$limit" "$@" > "gpurun_out/$name.log" 2>&1
-    local rc=$?
-    echo "== $name rc=$rc: $(grep -v amdgpu.ids "gpurun_out/$name.log" | tail -n 1 | cut -c1-220)"
-    if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-    return 0
-}
-step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
-step pytest_gpu 600 python -u -m pytest tests -m gpu -q --timeout 120 --timeout-method thread
-step bench_C2 300 python bench.py
-for c in C3 C4 C5; do step bench_$c 300 python bench.py --config $c --no-cpu-baseline; done
-DIST_RUNS="tiles:64 rgb24:8" step dist 300 bash tools/dist_rehearsal.sh
-cat gpurun_out/dist.log
+# Round-end check of the product build on one MI355X (GPU box, through gpurun):
+#   bash tools/round_check.sh OUT_DIR [steps]
+# the GPU suite, smoke, the driver's own bench command (--gpus 1 --steps 20 --warmup 5) and the default
+# bench line (1024 frames, also C2/C4/C5, CPU baseline, Tick rates), each under its own time limit; prints
+# one summary line per bench run.  (Round 4's one-off drivers tools/rounds/r04b.sh ... r04z.sh, which the
+# r04 profiles cite, were this script with fixed output directories; git history keeps them.)
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-/root/repo}
+cd $R
+O=${1:-gpurun_out/check}
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu.log 2>&1 \
+    || { echo "GPU TESTS FAILED"; tail -30 $O/gpu.log; exit 1; }
+echo "gpu tests: $(tail -1 $O/gpu.log)"
+timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }
+echo "smoke: $(tail -1 $O/smoke.log)"
+timeout -k 10 400 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/driver.json 2> $O/driver.err || { tail $O/driver.err; exit 1; }
+timeout -k 10 500 python bench.py ${2:+--steps $2} > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 1; }
+for f in driver bench; do
+python3 - $O/$f.json $f <<'PY'
+import json, sys
+d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
+w = d["config"]["workload"].split(":")[0]
+print(sys.argv[2], w, round(d["value"] / 1e3, 1), "Gray/s", round(d["ms_per_step"] * 1e3, 2), "us/frame; single",
+      round(d.get("single_launch_fps", 0)), "tick", round(d.get("tick_fps_incl_d2h", 0)), "async",
+      round(d.get("tick_async_fps_incl_d2h", 0)), "roofline", round(d["roofline"]["frac"], 4), "valu",
+      round(d["roofline_valu"]["frac"] or 0, 3), "order", d.get("dispatch_order"))
+for k, v in d.get("also", {}).items():
+    print("  ", k, round(v["value"] / 1e3, 1), "Gray/s", round(v["ms_per_step"] * 1e3, 2), "us/frame")
+for k, v in (d.get("tick_by_config") or {}).items():
+    if isinstance(v, dict):
+        print("   tick", k, round(v["tick_fps"], 1), "fps sync", round(v["tick_async_fps"], 1), "async",
+              round(v["tick_d2h_gbs"], 1), "GB/s")
+c = d["cpu_baseline"]
+print("   cpu", round(c["value"], 1), c["frame_ms_p10_p50_p90"], c["cpus_scheduled"], c["cgroup_throttled"])
+PY
+done

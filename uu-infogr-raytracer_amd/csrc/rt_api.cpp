@@ -783,15 +783,30 @@ int flush_hand(rt_ctx* ctx) {
     return RT_OK;
 }
 
-// A worker's band set (src, packed) into an unregistered (or unmapped) host frame: the runtime's
-// copies, one per band (n > 1) -- the slow path; callers register Surface.pixels once.  (A pitched
-// 2-D copy into pageable memory is not used: nothing bounds what its staging writes past the last row.)
-int runtime_band_copy(rt_ctx* ctx, const Share& sh, int W, int H, const int32_t* src, int32_t* host, hipStream_t st) {
+// A worker's band set (src, packed) into the host frame by the runtime's copies: one contiguous copy
+// (one worker), a pitched 2-D copy over the whole bands plus the frame's cut last band (a registered,
+// pinned frame: the copy engine writes the rows in place), or one copy per band (an unregistered frame
+// -- the slow path; callers register Surface.pixels once -- where a pitched copy would be staged).
+int runtime_band_copy(rt_ctx* ctx, const Share& sh, int W, int H, const int32_t* src, int32_t* host, hipStream_t st,
+                      bool pinned = false) {
     if (sh.nb <= 0) return RT_OK;
     const size_t bw = (size_t)sh.band_rows * (size_t)W;
     if (sh.step == 1) {
         HIP_TRY(ctx, hipMemcpyAsync(host + (size_t)sh.first * bw, src, sh.words * sizeof(int32_t),
                                     hipMemcpyDeviceToHost, st));
+        return RT_OK;
+    }
+    if (pinned) {
+        const bool cut = share_words(sh, W, H, sh.nb - 1, sh.nb) < bw;
+        const int full = sh.nb - (cut ? 1 : 0);
+        if (full > 0)
+            HIP_TRY(ctx, hipMemcpy2DAsync(host + (size_t)sh.first * bw, (size_t)sh.step * bw * sizeof(int32_t), src,
+                                          bw * sizeof(int32_t), bw * sizeof(int32_t), (size_t)full,
+                                          hipMemcpyDeviceToHost, st));
+        if (cut)
+            HIP_TRY(ctx, hipMemcpyAsync(host + (size_t)(sh.first + (size_t)full * sh.step) * bw, src + (size_t)full * bw,
+                                        share_words(sh, W, H, full, sh.nb) * sizeof(int32_t), hipMemcpyDeviceToHost,
+                                        st));
         return RT_OK;
     }
     for (int k = 0; k < sh.nb; ++k)
@@ -1658,7 +1673,8 @@ int rt_comm_gather(rt_ctx* ctx, const void* d_send, size_t n_bytes, void* d_recv
 int rt_register_host(rt_ctx* ctx, void* host_ptr, size_t bytes) {
     if (!ctx || !host_ptr || !bytes) return fail(ctx, RT_ERR_INVALID_ARG, "rt_register_host: bad arguments");
     DeviceGuard guard(ctx->dev[0].id);
-    // mapped into every device's address space: each worker's copy kernel writes its own bands
+    // mapped into every device's address space: each worker's copy kernel writes its own bands (a
+    // coarse-grained lock, hipExtHostRegisterCoarseGrained, measured the same copy rates: r05f)
     hipError_t e = hipHostRegister(host_ptr, bytes, hipHostRegisterMapped | hipHostRegisterPortable);
     if (e != hipSuccess) {
         (void)hipGetLastError();
@@ -1697,6 +1713,14 @@ namespace {
 // copy of chunk c rides in the launch of chunk c + 1 (the last one by the copy kernel alone), so the
 // PCIe-bound copy runs under the trace instead of after it.  RT_TICK_CHUNKS=1..8 fixes the count;
 // by default it grows with the share (a chunk of ~4 M pixels or more: a 1080p frame is one chunk).
+// How a registered frame's hand-off is copied in the synchronous Tick: RT_TICK_COPY=runtime (the runtime's
+// copy engine: contiguous / pitched copies after the trace) or kernel (the copy kernel through the
+// device-mapped address, chunked); default: the runtime's for one worker.
+bool tick_copy_kernel(const rt_ctx* ctx) {
+    if (const char* e = std::getenv("RT_TICK_COPY")) return std::strcmp(e, "kernel") == 0;
+    return ctx->n_gpus > 1;
+}
+
 int tick_chunks(const rt_ctx* ctx, int W, int H) {
     if (const char* e = std::getenv("RT_TICK_CHUNKS")) {
         const int k = std::atoi(e);
@@ -1716,16 +1740,17 @@ int tick_sync(rt_ctx* ctx, int W, int H, int32_t* pixels) {
         Device& d = ctx->dev[(size_t)g];
         DeviceGuard guard(d.id);
         int32_t* mapped = mapped_host(ctx, g, pixels, frame_bytes);
-        const int nc = mapped ? chunks : 1;
+        const bool kernel_copy = mapped && tick_copy_kernel(ctx);
+        const int nc = kernel_copy ? chunks : 1;
         const Share sh = share_of(W, H, g, n, nc > 1);
         if (sh.nb <= 0) continue;
         int rc = grow(ctx, (void**)&d.d_bands, &d.bands_cap, (size_t)sh.nb * sh.band_rows * W * sizeof(int32_t));
         if (rc != RT_OK) return rc;
-        if (!mapped || (n == 1 && nc == 1)) {  // unregistered, or the whole frame on one device: runtime's copy
+        if (!kernel_copy || (n == 1 && nc == 1)) {  // the runtime's copies after the trace
             rc = trace_bands(ctx, d, d.stream, W, H, sh.band_rows, sh.first, sh.step, d.d_bands, nullptr);
             if (rc != RT_OK) return rc;
             const bool ctimed = begin_timed(ctx, d, 1);
-            rc = runtime_band_copy(ctx, sh, W, H, d.d_bands, pixels, d.stream);
+            rc = runtime_band_copy(ctx, sh, W, H, d.d_bands, pixels, d.stream, mapped != nullptr);
             end_timed(d, ctimed);
             if (rc != RT_OK) return rc;
             continue;
