@@ -46,18 +46,34 @@ def _stats(ctx):
     return {k: st[k] for k in ("primary_rays", "reflect_rays", "shadow_rays")}
 
 
-@pytest.fixture
-def chunks_env():
-    """Set RT_TICK_CHUNKS for one test (read by every rt_render), restored afterwards."""
-    old = os.environ.get("RT_TICK_CHUNKS")
+def _env_fixture(name):
+    old = os.environ.get(name)
 
     def set_(v):
         if v is None:
-            os.environ.pop("RT_TICK_CHUNKS", None)
+            os.environ.pop(name, None)
         else:
-            os.environ["RT_TICK_CHUNKS"] = str(v)
+            os.environ[name] = str(v)
     yield set_
     set_(old)
+
+
+@pytest.fixture
+def chunks_env():
+    """Set RT_TICK_CHUNKS for one test (read by every rt_render), restored afterwards."""
+    yield from _env_fixture("RT_TICK_CHUNKS")
+
+
+@pytest.fixture
+def copy_env():
+    """Set RT_TICK_COPY (the synchronous hand-off: runtime / kernel / stream) for one test."""
+    yield from _env_fixture("RT_TICK_COPY")
+
+
+@pytest.fixture
+def async_env():
+    """Set RT_TICK_ASYNC (rt_render_async's hand-off: copy slice / copy engine on a second stream)."""
+    yield from _env_fixture("RT_TICK_ASYNC")
 
 
 @pytest.mark.parametrize("cid", ["C2", "C3", "C5"])
@@ -104,14 +120,17 @@ def test_tick_workers_golden(golden, cid, world):
             ctx.unregister_host(px)
 
 
+@pytest.mark.parametrize("mode", [None, "kernel", "runtime"])
 @pytest.mark.parametrize("cid,world,chunks", [("C4", 1, None), ("C4", 2, 3), ("C4", 8, None), ("C5", 1, None),
                                               ("C5", 1, 3), ("C5", 2, None), ("C5", 8, 2), ("C2", 1, 4),
                                               ("C3", 3, 5)])
-def test_tick_chunked_golden(golden, chunks_env, cid, world, chunks):
-    """The synchronous Tick's chunked hand-off (a worker's bands in several launches, chunk c's copy riding
-    in chunk c+1's launch, the last by the copy kernel): the default chunk count (by share size: C5 at
-    n = 1 takes 4) and forced counts, including more chunks than a worker has bands."""
+def test_tick_chunked_golden(golden, chunks_env, copy_env, cid, world, chunks, mode):
+    """The synchronous Tick's chunked hand-off -- default: chunk c traced, then copied by the copy engine on
+    a second stream while chunk c+1 is traced; kernel: chunk c's copy rides in chunk c+1's launch, the last
+    by the copy kernel; runtime: one copy after the trace -- with the default chunk count (by share size:
+    C5 at n = 1 takes 8) and forced counts, including more chunks than a worker has bands."""
     chunks_env(chunks)
+    copy_env(mode)
     e = golden["cases"][cid]
     sc = scenes.config(cid)
     with Context(world, abi.RT_CREATE_SHARED_DEVICE) as ctx:
@@ -168,11 +187,14 @@ def test_tick_ragged_vs_oracle(oracle, chunks_env, size, world, registered):
             check_guard(buf)
 
 
+@pytest.mark.parametrize("mode", [None, "slice", "stream"])
 @pytest.mark.parametrize("world", [1, 2, 4, 7])
-def test_tick_async_workers_vs_oracle(oracle, world):
+def test_tick_async_workers_vs_oracle(oracle, async_env, world, mode):
     """rt_render_async at n workers: 7 frames queued, a new camera each and the frame size changing twice
     mid-queue, each into its own registered buffer, ONE rt_wait -- every frame = the oracle's.  Every
-    worker double-buffers its band set on its own stream; frame k's copy rides in frame k+1's launch."""
+    worker double-buffers its band set on its own stream; frame k's copy rides in frame k+1's launch (slice)
+    or runs on the copy engine behind frame k's trace (stream; the default for large shares)."""
+    async_env(mode)
     base = scenes.config("C3")
     sizes = [(320, 180)] * 3 + [(200, 113)] * 2 + [(320, 180)] * 2
     rng = np.random.default_rng(7)
@@ -207,10 +229,12 @@ def test_tick_async_workers_vs_oracle(oracle, world):
             check_guard(gb)
 
 
+@pytest.mark.parametrize("mode", [None, "slice", "stream"])
 @pytest.mark.parametrize("cid", ["C3", "C5"])
-def test_tick_async_workers_golden(golden, cid):
+def test_tick_async_workers_golden(golden, async_env, cid, mode):
     """Full-size double-buffered Ticks at 4 workers, two frames deep with a wait per pair (the display
     loop of bench.py's tick_async_*): both buffers = the golden frame after each wait."""
+    async_env(mode)
     e = golden["cases"][cid]
     sc = scenes.config(cid)
     with Context(4, abi.RT_CREATE_SHARED_DEVICE) as ctx:

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--chunks", default="", help="comma list of RT_TICK_CHUNKS values ('' = the default)")
     ap.add_argument("--shared", action="store_true")
     ap.add_argument("--copy", default="", help="RT_TICK_COPY for the run: runtime | kernel ('' = the library's default)")
+    ap.add_argument("--async-copy", default="", help="RT_TICK_ASYNC for the run: stream | slice ('' = default)")
     ap.add_argument("--frames", type=int, default=20)
     ap.add_argument("--reps", type=int, default=3)
     a = ap.parse_args()
@@ -27,6 +28,8 @@ def main():
     from raytracer_hip import Context, abi, scenes
     if a.copy:
         os.environ["RT_TICK_COPY"] = a.copy
+    if a.async_copy:
+        os.environ["RT_TICK_ASYNC"] = a.async_copy
     for cid in a.configs.split(","):
         sc = scenes.config(cid)
         W, H = sc.width, sc.height
@@ -62,7 +65,7 @@ def main():
                         rates.append(a.frames / (time.perf_counter() - t))
                     r = sorted(rates)[len(rates) // 2]
                     out.append(f"{name} {r:8.1f} fps ({W * H * 4 * r / 1e9:6.1f} GB/s of frame)")
-                print(f"{cid} world {world}{' shared' if a.shared else ''} copy {a.copy or 'default'} chunks "
+                print(f"{cid} world {world}{' shared' if a.shared else ''} copy {a.copy or 'default'}/{a.async_copy or 'default'} chunks "
                       f"{ch or 'default'}: " + "; ".join(out),
                       flush=True)
             for b in bufs:

@@ -144,6 +144,12 @@ struct Device {
         CopyJob job{};            // the band set -> the buffer's device-mapped address (job.words 0: none)
     } hand;
     hipEvent_t ev_join = nullptr;  // rt_render_device at n > 1: ordering against the caller's stream
+    // the synchronous Tick's copy-engine hand-off of chunk c on its own stream, after the chunk's trace
+    hipStream_t copy_stream = nullptr;
+    hipEvent_t ev_chunk[8] = {};
+    // rt_render_async's copy-engine hand-off (RT_TICK_ASYNC=stream): slot s traced -> copied events
+    hipEvent_t ev_traced[2] = {}, ev_copied[2] = {};
+    bool copy_pending[2] = {false, false};
     float* d_view_tab = nullptr;  // lx[W] then ly[H] (view_tables)
     size_t view_tab_cap = 0;
     int tab_w = -1, tab_h = -1;
@@ -182,6 +188,7 @@ struct SceneLayout {
     bool has_shg = false;  // per-light shadow grids (DevShadowGrid) for the merged shadow pass
     std::vector<unsigned char> host_blob;  // the uploaded scene image (host tests read the tables)
     bool generic_pow = false;        // a specular material with n not in {0.5, 1, 2}
+    bool lights_a2_ok = true;        // every light's 2a = 2 p.p finite and > 0
     std::vector<DevSphere> host_sph;  // for the per-frame primary constants
     std::vector<DevPlane> host_pl;    // for the single-frame launches' row order (row_order)
 };
@@ -522,6 +529,7 @@ void scene_params(const rt_ctx* ctx, const Device& d, LaunchParams& lp) {
     lp.shgrid = L.has_shg ? (const unsigned long long*)(base + L.off_shgrid) : nullptr;
     lp.shslab = L.has_shg ? (const unsigned long long*)(base + L.off_shslab) : nullptr;
     lp.S = L.S, lp.P = L.P, lp.L = L.L, lp.limit = L.limit;
+    lp.lights_a2_ok = L.lights_a2_ok ? 1 : 0;
     lp.counters = d.d_counters;
 }
 
@@ -788,30 +796,31 @@ int flush_hand(rt_ctx* ctx) {
 // pinned frame: the copy engine writes the rows in place), or one copy per band (an unregistered frame
 // -- the slow path; callers register Surface.pixels once -- where a pitched copy would be staged).
 int runtime_band_copy(rt_ctx* ctx, const Share& sh, int W, int H, const int32_t* src, int32_t* host, hipStream_t st,
-                      bool pinned = false) {
-    if (sh.nb <= 0) return RT_OK;
+                      bool pinned = false, int k0 = 0, int k1 = -1) {
+    if (k1 < 0) k1 = sh.nb;  // bands [k0, k1) of the share; src = the packed band set (band 0)
+    if (k1 <= k0) return RT_OK;
     const size_t bw = (size_t)sh.band_rows * (size_t)W;
+    auto dst = [&](int k) { return host + (size_t)(sh.first + (size_t)k * sh.step) * bw; };
     if (sh.step == 1) {
-        HIP_TRY(ctx, hipMemcpyAsync(host + (size_t)sh.first * bw, src, sh.words * sizeof(int32_t),
+        HIP_TRY(ctx, hipMemcpyAsync(dst(k0), src + (size_t)k0 * bw, share_words(sh, W, H, k0, k1) * sizeof(int32_t),
                                     hipMemcpyDeviceToHost, st));
         return RT_OK;
     }
     if (pinned) {
-        const bool cut = share_words(sh, W, H, sh.nb - 1, sh.nb) < bw;
-        const int full = sh.nb - (cut ? 1 : 0);
+        const bool cut = share_words(sh, W, H, k1 - 1, k1) < bw;
+        const int full = k1 - k0 - (cut ? 1 : 0);
         if (full > 0)
-            HIP_TRY(ctx, hipMemcpy2DAsync(host + (size_t)sh.first * bw, (size_t)sh.step * bw * sizeof(int32_t), src,
+            HIP_TRY(ctx, hipMemcpy2DAsync(dst(k0), (size_t)sh.step * bw * sizeof(int32_t), src + (size_t)k0 * bw,
                                           bw * sizeof(int32_t), bw * sizeof(int32_t), (size_t)full,
                                           hipMemcpyDeviceToHost, st));
         if (cut)
-            HIP_TRY(ctx, hipMemcpyAsync(host + (size_t)(sh.first + (size_t)full * sh.step) * bw, src + (size_t)full * bw,
-                                        share_words(sh, W, H, full, sh.nb) * sizeof(int32_t), hipMemcpyDeviceToHost,
-                                        st));
+            HIP_TRY(ctx, hipMemcpyAsync(dst(k1 - 1), src + (size_t)(k1 - 1) * bw,
+                                        share_words(sh, W, H, k1 - 1, k1) * sizeof(int32_t), hipMemcpyDeviceToHost, st));
         return RT_OK;
     }
-    for (int k = 0; k < sh.nb; ++k)
-        HIP_TRY(ctx, hipMemcpyAsync(host + (size_t)(sh.first + (size_t)k * sh.step) * bw, src + (size_t)k * bw,
-                                    share_words(sh, W, H, k, k + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+    for (int k = k0; k < k1; ++k)
+        HIP_TRY(ctx, hipMemcpyAsync(dst(k), src + (size_t)k * bw, share_words(sh, W, H, k, k + 1) * sizeof(int32_t),
+                                    hipMemcpyDeviceToHost, st));
     return RT_OK;
 }
 
@@ -976,6 +985,13 @@ void rt_destroy(rt_ctx* ctx) {
         for (auto* v : {&d.order.pending, &d.order.pool})
             for (Device::OrderTuner::Probe& pr : *v) (void)hipEventDestroy(pr.a), (void)hipEventDestroy(pr.b);
         if (d.ev_join) (void)hipEventDestroy(d.ev_join);
+        for (hipEvent_t& ev : d.ev_chunk)
+            if (ev) (void)hipEventDestroy(ev);
+        for (int i = 0; i < 2; ++i) {
+            if (d.ev_traced[i]) (void)hipEventDestroy(d.ev_traced[i]);
+            if (d.ev_copied[i]) (void)hipEventDestroy(d.ev_copied[i]);
+        }
+        if (d.copy_stream) (void)hipStreamDestroy(d.copy_stream);
         if (d.comm && g_rccl.CommDestroy) (void)g_rccl.CommDestroy(d.comm);
         if (d.d_scene) (void)hipFree(d.d_scene);
         if (d.d_frame) (void)hipFree(d.d_frame);
@@ -1210,6 +1226,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
         d.a2 = 2.0f * d.a;
         d.a4 = 4.0f * d.a;
         d.sh_t = shadow_threshold(d.a2);  // used only when a2 is finite and > 0 (wave-uniform per light)
+        if (!(d.a2 > 0.0f && d.a2 < INFINITY)) L.lights_a2_ok = false;
         // shadow-cull frame (kernel uses it only when a is in [2^-40, 2^40])
         const double len = std::sqrt((double)p.x * p.x + (double)p.y * p.y + (double)p.z * p.z);
         double A[3] = {0.0, 0.0, 1.0};
@@ -1709,25 +1726,33 @@ int rt_unregister_host(rt_ctx* ctx, void* host_ptr) {
 }
 
 namespace {
-// Chunks of a worker's share in a synchronous Tick: its bands are traced in `chunks` launches and the
-// copy of chunk c rides in the launch of chunk c + 1 (the last one by the copy kernel alone), so the
-// PCIe-bound copy runs under the trace instead of after it.  RT_TICK_CHUNKS=1..8 fixes the count;
-// by default it grows with the share (a chunk of ~4 M pixels or more: a 1080p frame is one chunk).
-// How a registered frame's hand-off is copied in the synchronous Tick: RT_TICK_COPY=runtime (the runtime's
-// copy engine: contiguous / pitched copies after the trace) or kernel (the copy kernel through the
-// device-mapped address, chunked); default: the runtime's for one worker.
-bool tick_copy_kernel(const rt_ctx* ctx) {
-    if (const char* e = std::getenv("RT_TICK_COPY")) return std::strcmp(e, "kernel") == 0;
-    return ctx->n_gpus > 1;
+// How a registered frame's hand-off is copied in the synchronous Tick (RT_TICK_COPY): runtime -- the
+// runtime's copy engine after the trace, same stream; kernel -- the copy kernel through the device-mapped
+// address, chunked (chunk c's copy rides in chunk c+1's launch, the last by the copy kernel alone);
+// stream -- chunked, each chunk's copy by the copy engine on a second stream after the chunk's trace
+// (event-ordered), so it runs under the next chunk's trace.  Default: stream (r05k, one GPU: C5 271 ->
+// 391 fps at 4 chunks, C4 1,028 -> 1,250; the copy kernel writes host memory at ~35 GB/s against the
+// copy engine's ~52).  A share of one chunk (a 1080p frame) takes the runtime's copy after the trace at
+// n = 1 and the copy kernel at n > 1, whose bands are too short for pitched copies.
+enum TickCopy { TICK_RUNTIME = 0, TICK_KERNEL = 1, TICK_STREAM = 2 };
+TickCopy tick_copy_mode() {
+    if (const char* e = std::getenv("RT_TICK_COPY")) {
+        if (std::strcmp(e, "kernel") == 0) return TICK_KERNEL;
+        if (std::strcmp(e, "runtime") == 0) return TICK_RUNTIME;
+    }
+    return TICK_STREAM;
 }
 
+// Chunks of a worker's share in a synchronous Tick.  RT_TICK_CHUNKS=1..8 fixes the count; by default one
+// chunk per ~2 M pixels of the share, at most 8 (1080p: 1; C4 at n = 1: 4; C5: 8 at n = 1, 2 at n = 8;
+// r05k: C4 4 chunks 1,250 fps against 8 chunks 1,016, C5 8 chunks ~ 4).
 int tick_chunks(const rt_ctx* ctx, int W, int H) {
     if (const char* e = std::getenv("RT_TICK_CHUNKS")) {
         const int k = std::atoi(e);
         if (k >= 1 && k <= 8) return k;
     }
     const double share = (double)W * H / ctx->n_gpus;
-    return share >= 16e6 ? 4 : share >= 4e6 ? 2 : 1;
+    return (int)std::min(8.0, std::max(1.0, std::floor(share / 2.0e6 + 0.5)));
 }
 
 // The synchronous Tick of every worker: each traces its band set and copies it into `pixels` on its
@@ -1740,13 +1765,30 @@ int tick_sync(rt_ctx* ctx, int W, int H, int32_t* pixels) {
         Device& d = ctx->dev[(size_t)g];
         DeviceGuard guard(d.id);
         int32_t* mapped = mapped_host(ctx, g, pixels, frame_bytes);
-        const bool kernel_copy = mapped && tick_copy_kernel(ctx);
-        const int nc = kernel_copy ? chunks : 1;
+        const TickCopy mode = mapped ? tick_copy_mode() : TICK_RUNTIME;
+        const int nc = mode != TICK_RUNTIME ? chunks : 1;
         const Share sh = share_of(W, H, g, n, nc > 1);
         if (sh.nb <= 0) continue;
         int rc = grow(ctx, (void**)&d.d_bands, &d.bands_cap, (size_t)sh.nb * sh.band_rows * W * sizeof(int32_t));
         if (rc != RT_OK) return rc;
-        if (!kernel_copy || (n == 1 && nc == 1)) {  // the runtime's copies after the trace
+        if (mode == TICK_STREAM && nc > 1) {  // chunk c: trace (stream) -> event -> copy engine (copy stream)
+            if (!d.copy_stream) HIP_TRY(ctx, hipStreamCreateWithFlags(&d.copy_stream, hipStreamNonBlocking));
+            for (int c = 0; c < nc; ++c) {
+                const int k0 = (int)((long long)sh.nb * c / nc), k1 = (int)((long long)sh.nb * (c + 1) / nc);
+                if (k1 <= k0) continue;
+                if (!d.ev_chunk[c]) HIP_TRY(ctx, hipEventCreateWithFlags(&d.ev_chunk[c], hipEventDisableTiming));
+                rc = trace_bands(ctx, d, d.stream, W, H, sh.band_rows, sh.first + k0 * sh.step, sh.step,
+                                 d.d_bands + (size_t)k0 * sh.band_rows * W, nullptr, RT_BANDS_INT32, 1, 0, nullptr,
+                                 nullptr, k1 - k0);
+                if (rc != RT_OK) return rc;
+                HIP_TRY(ctx, hipEventRecord(d.ev_chunk[c], d.stream));
+                HIP_TRY(ctx, hipStreamWaitEvent(d.copy_stream, d.ev_chunk[c], 0));
+                rc = runtime_band_copy(ctx, sh, W, H, d.d_bands, pixels, d.copy_stream, true, k0, k1);
+                if (rc != RT_OK) return rc;
+            }
+            continue;
+        }
+        if (mode == TICK_RUNTIME || (nc == 1 && n == 1)) {  // the runtime's copy after the trace
             rc = trace_bands(ctx, d, d.stream, W, H, sh.band_rows, sh.first, sh.step, d.d_bands, nullptr);
             if (rc != RT_OK) return rc;
             const bool ctimed = begin_timed(ctx, d, 1);
@@ -1773,6 +1815,7 @@ int tick_sync(rt_ctx* ctx, int W, int H, int32_t* pixels) {
     for (Device& d : ctx->dev) {
         DeviceGuard guard(d.id);
         HIP_TRY(ctx, hipStreamSynchronize(d.stream));
+        if (d.copy_stream) HIP_TRY(ctx, hipStreamSynchronize(d.copy_stream));
     }
     return RT_OK;
 }
@@ -1784,8 +1827,8 @@ int rt_render(rt_ctx* ctx, int width, int height, int32_t* pixels) {
     if (rc != RT_OK) return rc;
     if (!pixels) return fail(ctx, RT_ERR_INVALID_ARG, "NULL pixels");
     for (const Device& d : ctx->dev)
-        if (d.hand.job.words) {  // rt_render_async frames first (the caller may reuse their buffers)
-            rc = rt_wait(ctx);
+        if (d.hand.job.words || d.copy_pending[0] || d.copy_pending[1]) {  // rt_render_async frames first (the
+            rc = rt_wait(ctx);                                             // caller may reuse their buffers)
             if (rc != RT_OK) return rc;
             break;
         }
@@ -1831,21 +1874,61 @@ int rt_render_async(rt_ctx* ctx, int width, int height, int32_t* pixels) {
     if (ctx->rccl_gather) return rt_render(ctx, width, height, pixels);
     const size_t frame_bytes = (size_t)width * height * sizeof(int32_t);
     const int n = ctx->n_gpus;
+    // The hand-off of frame k: by the copy engine on a second stream, chunk by chunk after each chunk's trace
+    // (event-ordered; the trace of frame k+2 into the same buffer waits for the copy), or as the copy slice
+    // in frame k+1's launch.  Default (RT_TICK_ASYNC=stream|slice overrides): the copy engine, except for
+    // shares under 0.5 M pixels at n > 1, whose short bands the pitched copies move slowly (r05l, one GPU,
+    // two frames deep: C3 4,928 -> 5,167 fps, C4 1,034 -> 1,261, C5 268 -> 331; C2 at 8 workers 4,800 ->
+    // 4,338 with the engine).
+    const char* am = std::getenv("RT_TICK_ASYNC");
+    const bool engine = am ? std::strcmp(am, "stream") == 0 : (n == 1 || (double)width * height / n >= 5e5);
+    const int nc = engine ? tick_chunks(ctx, width, height) : 1;
     for (int g = 0; g < n; ++g) {
         Device& d = ctx->dev[(size_t)g];
         DeviceGuard guard(d.id);
         if (!d.async_stream) HIP_TRY(ctx, hipStreamCreateWithFlags(&d.async_stream, hipStreamNonBlocking));
         const int slot = d.async_next;
-        const Share sh = share_of(width, height, g, n, false);
+        const Share sh = share_of(width, height, g, n, nc > 1);
         const size_t bytes = std::max<size_t>(1, (size_t)sh.nb * sh.band_rows * width) * sizeof(int32_t);
         if (d.frames2_cap[slot] < bytes || sh.nb <= 0) {  // (re)allocation: the pending copy may read the
             rc = flush_hand(ctx);                         // other buffer only, but nothing may still use
             if (rc != RT_OK) return rc;                   // this one
             HIP_TRY(ctx, hipStreamSynchronize(d.async_stream));
+            if (d.copy_stream) HIP_TRY(ctx, hipStreamSynchronize(d.copy_stream));
+            d.copy_pending[0] = d.copy_pending[1] = false;
         }
         if (sh.nb <= 0) continue;  // (more workers than bands)
         rc = grow(ctx, (void**)&d.d_frames2[slot], &d.frames2_cap[slot], bytes);
         if (rc != RT_OK) return rc;
+        if (engine) {
+            if (!d.copy_stream) HIP_TRY(ctx, hipStreamCreateWithFlags(&d.copy_stream, hipStreamNonBlocking));
+            for (int i = 0; i < 2; ++i) {
+                if (!d.ev_traced[i]) HIP_TRY(ctx, hipEventCreateWithFlags(&d.ev_traced[i], hipEventDisableTiming));
+                if (!d.ev_copied[i]) HIP_TRY(ctx, hipEventCreateWithFlags(&d.ev_copied[i], hipEventDisableTiming));
+            }
+            rc = flush_hand(ctx);  // (a slice-mode frame still pending)
+            if (rc != RT_OK) return rc;
+            if (d.copy_pending[slot]) HIP_TRY(ctx, hipStreamWaitEvent(d.async_stream, d.ev_copied[slot], 0));
+            const bool pinned = mapped_host(ctx, g, pixels, frame_bytes) != nullptr;
+            for (int c = 0; c < nc; ++c) {
+                const int k0 = (int)((long long)sh.nb * c / nc), k1 = (int)((long long)sh.nb * (c + 1) / nc);
+                if (k1 <= k0) continue;
+                hipEvent_t& ev = nc > 1 ? d.ev_chunk[c] : d.ev_traced[slot];
+                if (!ev) HIP_TRY(ctx, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+                rc = trace_bands(ctx, d, d.async_stream, width, height, sh.band_rows, sh.first + k0 * sh.step, sh.step,
+                                 d.d_frames2[slot] + (size_t)k0 * sh.band_rows * width, nullptr, RT_BANDS_INT32, 1, 0,
+                                 nullptr, nullptr, k1 - k0);
+                if (rc != RT_OK) return rc;
+                HIP_TRY(ctx, hipEventRecord(ev, d.async_stream));
+                HIP_TRY(ctx, hipStreamWaitEvent(d.copy_stream, ev, 0));
+                rc = runtime_band_copy(ctx, sh, width, height, d.d_frames2[slot], pixels, d.copy_stream, pinned, k0, k1);
+                if (rc != RT_OK) return rc;
+            }
+            HIP_TRY(ctx, hipEventRecord(d.ev_copied[slot], d.copy_stream));
+            d.copy_pending[slot] = true;
+            d.async_next = slot ^ 1;
+            continue;
+        }
         rc = trace_bands(ctx, d, d.async_stream, width, height, sh.band_rows, sh.first, sh.step, d.d_frames2[slot],
                          nullptr, RT_BANDS_INT32, 1, 0, nullptr, d.hand.job.words ? &d.hand.job : nullptr);
         if (rc != RT_OK) return rc;
@@ -1873,6 +1956,8 @@ int rt_wait(rt_ctx* ctx) {
         DeviceGuard guard(d.id);
         HIP_TRY(ctx, hipStreamSynchronize(d.stream));
         if (d.async_stream) HIP_TRY(ctx, hipStreamSynchronize(d.async_stream));
+        if (d.copy_stream) HIP_TRY(ctx, hipStreamSynchronize(d.copy_stream));
+        d.copy_pending[0] = d.copy_pending[1] = false;
     }
     return RT_OK;
 }

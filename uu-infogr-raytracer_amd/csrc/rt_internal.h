@@ -156,6 +156,7 @@ struct LaunchParams {
     const float* lxt;  // [W]: ((float)x / W - 0.5f) * pw, TracePixel :963-965
     const float* lyt;  // [H]: ((float)y / H - 0.5f) * ph
     int S, P, L, limit;
+    int lights_a2_ok;  // every light's 2a = 2 p.p is finite and > 0 (the shadow loops' exact-threshold form)
     // view, RayTracer.cs:511-523 and :892-896 (computed on the host)
     float cam[3], right[3], up[3], fwd[3];
     float pw, ph, nearc;

@@ -547,6 +547,18 @@ __device__ __forceinline__ void take_secondary(float t, int i, float& best, int&
     win = b ? i : win;
 }
 
+// A plane test in a nearest-plane search (TracePixel :985-991, TraceSecondaryRay :819-821 -- the same rule):
+// t = num / den is selectable only when t > 0, i.e. num and den nonzero with equal signs (zeros give +-0,
+// +-inf or NaN, and +inf never beats the initial +inf); when no lane of the wave (of the active lanes, in
+// divergent code) has such a pair the division and the selection are skipped -- the upper half of a
+// frame for a floor, rays leaving a wall -- and otherwise every lane takes the literal quotient.
+__device__ __forceinline__ void plane_take(f3 o, f3 d, const DevPlane& q, int i, float& best, int& win) {
+    const float num = ((-o.x * q.nx - o.y * q.ny) - o.z * q.nz) + q.cn;
+    const float den = dot(d, mk(q.nx, q.ny, q.nz));
+    const bool may = (num > 0.0f && den > 0.0f) || (num < 0.0f && den < 0.0f);
+    if (__builtin_amdgcn_ballot_w64(may) != 0) take_primary(num / den, i, best, win);  // (wave-uniform)
+}
+
 // DIRECT path (scenes with < CULL_MIN_SPHERES spheres): per-lane divergent walks, wave-uniform
 // primitive loops.  Shading of one shaded hit (TraceSphere :847-873 / TracePlane :736-778): the
 // colour is accumulated in the reference's order -- mirror term (from the deeper segment `sec`),
@@ -750,7 +762,7 @@ __device__ __forceinline__ Hit nearest_direct(const LaunchParams& p, f3 o, f3 d,
     int win_p = -1;
     for (int i = 0; i < p.P; ++i) {
         tl.plane(true);
-        take_primary(plane_t(o, d, p.pl[i]), i, best_p, win_p);  // t > 0 && t < best (:985-991, :819-821)
+        plane_take(o, d, p.pl[i], i, best_p, win_p);  // t > 0 && t < best (:985-991, :819-821)
     }
     if (best_s < best_p) return Hit{best_s, win_s};
     if (win_p >= 0) return Hit{best_p, ~win_p};
@@ -769,7 +781,7 @@ __device__ __forceinline__ Hit terminal_direct(const LaunchParams& p, f3 o, f3 d
     int win_p = -1;
     for (int i = 0; i < p.P; ++i) {
         tl.plane(true);
-        take_primary(plane_t(o, d, p.pl[i]), i, best_p, win_p);
+        plane_take(o, d, p.pl[i], i, best_p, win_p);
     }
     if (win_p < 0 || !(best_p - 0.01f > 0.0f)) return Hit{0.0f, HIT_NONE};
     const float a = dot(d, d);
@@ -1167,7 +1179,7 @@ __device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d,
     } else {
         for (int i = 0; i < p.P; ++i) {
             tl.plane(active);
-            take_primary(plane_t(o, d, p.pl[i]), i, best_p, win_p);  // t > 0 && t < best
+            plane_take(o, d, p.pl[i], i, best_p, win_p);  // t > 0 && t < best
         }
     }
     if (!active) return Hit{0.0f, HIT_NONE};
@@ -1544,7 +1556,7 @@ __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int
             int win_p = -1;
             for (int i = 0; i < p.P; ++i) {
                 tl.plane(active);
-                take_primary(plane_t(o, d, p.pl[i]), i, best_p, win_p);  // t > 0 && t < best
+                plane_take(o, d, p.pl[i], i, best_p, win_p);  // t > 0 && t < best
             }
             const bool need = active && win_p >= 0 && best_p - 0.01f > 0.0f;
             h = Hit{0.0f, HIT_NONE};
