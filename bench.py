@@ -109,6 +109,11 @@ def parse(argv=None):
                     help="N>1 tiles: rank 0 traces nothing and assembles the frames that ranks 1..N-1 "
                          "trace as a band world of N-1 (auto: N >= 8, where rank 0's own share plus the "
                          "decode of the others' made it the slowest rank)")
+    ap.add_argument("--rank0-share", default="auto",
+                    help="N>1 tiles: rank 0's share of the frame -- auto: measured per leg (rank0_tail_rows: rank 0 "
+                         "renders the frame's last rows itself, sized so that its trace plus the decode of the others' "
+                         "bands take as long as their trace; 0 rows = the compositor, a share of 1/N or more = rank 0 "
+                         "as an ordinary band rank); off: --compositor decides; an integer: that many last rows")
     ap.add_argument("--torch-collectives", action="store_true",
                     help="N>1 tiles: the size reduce and the gather through torch.distributed (its own collective "
                          "stream, waited on side streams) also for a run of one batch, instead of the library's RCCL "
@@ -595,6 +600,57 @@ def auto_batch_frames(ctx, W, H, rb, band_rank, band_world, idle, steps, torch, 
     return -(-steps // k)
 
 
+# Rank 0's decode of the other ranks' wires per pixel of the frame (rt_decode_gathered; profiles/r04_dist_stages.txt:
+# 45.4 us for 20 C2 frames in one batch, 2.0-2.1 us per 1080p frame at 64 frames per batch)
+DECODE_S_PER_PX = 1.1e-12
+
+
+def rank0_tail_rows(ctx, W, H, band_rows, world, rank, torch, dist, log=None):
+    """Rank 0's share of an N > 1 leg (every rank takes part and gets the same answer): -1 = rank 0 is an
+    ordinary band rank (interleaved 1/N), 0 = compositor (rank 0 only decodes), h > 0 = rank 0 renders
+    the frame's last h rows (whole bands) itself and ranks 1..N-1 the rows above them.  Rank 0 measures
+    the full frame's trace T and the trace of a candidate tail t(h) (two-frame launches after a warm one)
+    and solves  t(h) + D (H - h) / H = (T - t(h)) / (N - 1)  for h with t(h) ~ c h (c from the probe,
+    refined once at the solution), D = the decode of a whole frame (DECODE_S_PER_PX).  A
+    solution at or above the uniform share 1/N keeps rank 0 interleaved."""
+    import time as _t
+    from raytracer_hip import abi as _abi
+    ans = torch.tensor([-1.0], dtype=torch.float64, device="cuda")
+    if rank == 0:
+        buf = torch.empty(2 * W * H, dtype=torch.int32, device="cuda")
+        st = torch.cuda.current_stream().cuda_stream
+
+        def probe(rows):  # two frames of the last `rows` rows (rows = H: the whole frame)
+            t = 0.0
+            for _ in range(2):
+                torch.cuda.synchronize()
+                t0 = _t.perf_counter()
+                ctx.render_bands_batch(W, H, band_rows, (H - rows) // band_rows, 1, 2, buf.data_ptr(), W * H * 4,
+                                       _abi.RT_BANDS_FRAME, st)
+                torch.cuda.synchronize()
+                t = (_t.perf_counter() - t0) / 2
+            return t
+        T = probe(H)
+        D = DECODE_S_PER_PX * W * H
+        hu = max(band_rows, (H // world) // band_rows * band_rows)  # the uniform share, whole bands
+        h, c = float(hu), probe(hu) / hu
+        for _ in range(2):  # the linear model, then once more with the slope measured at its solution
+            denom = c * world / (world - 1) - D / H
+            h = (T / (world - 1) - D) / denom if denom > 0 else 0.0
+            hb = int(h // band_rows) * band_rows
+            if hb <= 0 or hb >= hu:
+                break
+            c = probe(hb) / hb
+        hb = int(max(0.0, h) // band_rows) * band_rows
+        ans[0] = -1.0 if hb >= hu else float(hb)
+        if log:
+            log(f"rank 0 share: T {T * 1e6:.1f} us/frame, decode {D * 1e6:.1f} us/frame, tail slope "
+                f"{c * 1e9:.1f} ns/row, uniform {hu} rows -> {'interleaved' if hb >= hu else f'{hb} tail rows'}")
+        del buf
+    dist.all_reduce(ans, op=dist.ReduceOp.MAX) if world > 1 else None
+    return int(ans.item())
+
+
 def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, scenes, size=""):
     """One N > 1 measurement of `config_name` through the band pipeline (rank 0 returns the
     line's dict, the other ranks None).  Every rank runs every leg, so the collectives match."""
@@ -615,14 +671,28 @@ def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, s
     tg = None  # tile-encoded gather (--band-format tiles)
     run = None  # run(n): n steps (frames); else one step() per frame
     distributed = True
-    comp = False  # compositor mode (rank 0 only assembles)
+    comp = False  # compositor geometry (ranks 1..N-1 trace the frame, or all of it above rank 0's tail)
+    tail = 0      # rank 0's last rows (with comp): it renders them itself
+    Hc = H        # the band geometry's rows (H - tail)
     if True:
         from raytracer_hip.dist import BandGather, BatchedBandGather, RowBands
-        comp = (args.band_format == "tiles" and not args.no_pipeline and not args.rank0_codec and world >= 2
-                and (args.compositor == "on" or (args.compositor == "auto" and world >= 8)))
-        # band geometry: the process group's, or (compositor) ranks 1..N-1 as band ranks 0..N-2
+        tiles_ok = args.band_format == "tiles" and not args.no_pipeline and not args.rank0_codec and world >= 2
+        share = -1
+        if tiles_ok and args.rank0_share != "off":
+            share = (rank0_tail_rows(ctx, W, H, args.band_rows, world, rank, torch, dist,
+                                     lambda m: print(f"[{sc.name}] {m}", file=sys.stderr, flush=True))
+                     if args.rank0_share == "auto" else int(args.rank0_share))
+            comp = share >= 0
+            tail = max(0, share)
+        elif tiles_ok:
+            comp = args.compositor == "on" or (args.compositor == "auto" and world >= 8)
+        Hc = H - tail
+        # band geometry: the process group's, or (compositor) ranks 1..N-1 as band ranks 0..N-2 of the
+        # frame's first Hc rows, traced with the whole frame's view
         band_rank, band_world = (max(0, rank - 1), world - 1) if comp else (rank, world)
-        rb = RowBands(W, H, args.band_rows, band_rank, band_world)
+        if tail and rank > 0:
+            ctx.set_view_height(H)
+        rb = RowBands(W, Hc, args.band_rows, band_rank, band_world)
         launch_frames = 1
         px_per_launch = rb.pixels
         frame = torch.empty(W * H, dtype=torch.int32, device="cuda") if rank == 0 else None
@@ -647,19 +717,20 @@ def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, s
 
             def t_encode(raw, n, wire, size, st):
                 if raw is None:  # fused: the batch was traced into the wire; finish it
-                    ctx.finish_wire(W, H, rb.band_rows, band_rank, band_world, n, wire.data_ptr(), size.data_ptr(),
+                    ctx.finish_wire(W, Hc, rb.band_rows, band_rank, band_world, n, wire.data_ptr(), size.data_ptr(),
                                     st.cuda_stream)
                 else:
-                    ctx.encode_bands(W, H, rb.band_rows, band_rank, band_world, raw.data_ptr(), rb.slot_elems, n,
+                    ctx.encode_bands(W, Hc, rb.band_rows, band_rank, band_world, raw.data_ptr(), rb.slot_elems, n,
                                      wire.data_ptr(), size.data_ptr(), st.cuda_stream)
 
             def t_decode(recv, rank_stride, n, frames_, st, first_rank):
-                ctx.decode_gathered(W, H, rb.band_rows, band_world, recv.data_ptr(), rank_stride, n, frames_.data_ptr(),
-                                    W * H, st.cuda_stream, first_rank=first_rank)
+                # (rows [0, Hc) of each W x H frame: the band geometry's; rank 0 renders any rows below)
+                ctx.decode_gathered(W, Hc, rb.band_rows, band_world, recv.data_ptr(), rank_stride, n,
+                                    frames_.data_ptr(), W * H, st.cuda_stream, first_rank=first_rank)
 
             batch = args.batch
             if args.auto_batch and args.steps <= 128:
-                batch = auto_batch_frames(ctx, W, H, rb, band_rank, band_world, comp and rank == 0, args.steps,
+                batch = auto_batch_frames(ctx, W, Hc, rb, band_rank, band_world, comp and rank == 0, args.steps,
                                           torch, dist)
             coll = None
             if not args.rehearse_gloo and not args.torch_collectives and batch >= args.steps:
@@ -683,9 +754,9 @@ def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, s
                 if agree_min(1 if coll is not None else 0) == 0:  # one choice for every rank
                     coll = None
             tg = TileBandGather(rb, torch.device("cuda", local), batch,
-                                lambda n: wire_layout(W, H, rb.band_rows, band_world, n), t_encode, t_decode,
+                                lambda n: wire_layout(W, Hc, rb.band_rows, band_world, n), t_encode, t_decode,
                                 rank0_codec=args.rank0_codec, compositor=comp, phys_rank=rank, phys_world=world,
-                                fused=not args.no_fuse, coll=coll, main_stream=stream)
+                                fused=not args.no_fuse, coll=coll, main_stream=stream, tail_rows=tail)
             out_fmt = abi.RT_BANDS_FRAME if tg.direct else abi.RT_BANDS_INT32
             # frames alternate between trace streams (two in flight per rank); at a batch end the
             # encode runs on `stream` after the others joined it, and the trace streams then wait
@@ -695,7 +766,7 @@ def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, s
             tstreams = [stream] + [torch.cuda.Stream() for _ in range(max(1, args.inflight) - 1)]
             stride_b = (W * H if tg.direct else rb.slot_elems) * 4
             launch_frames = tg.F
-            px_per_launch = tg.F * rb.pixels
+            px_per_launch = tg.F * (tail * W if (tail and rank == 0) else rb.pixels)
             if rank == 0:
                 frame = None  # the decoded frames live in tg.frames (rings of F)
 
@@ -712,8 +783,11 @@ def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, s
                     if tg.k % tg.F == 0:
                         tg.begin_batch([ts])
                     if tg.fused:  # straight into the batch's wire (tile headers + codec scratch)
-                        ctx.render_bands_tiles(W, H, rb.band_rows, band_rank, band_world, tg.k % tg.F, m, tg.F,
+                        ctx.render_bands_tiles(W, Hc, rb.band_rows, band_rank, band_world, tg.k % tg.F, m, tg.F,
                                                tg.wire_target().data_ptr(), ts.cuda_stream)
+                    elif tail and rank == 0:  # rank 0's share: the frame's last `tail` rows, into its frames
+                        ctx.render_bands_batch(W, H, rb.band_rows, Hc // rb.band_rows, 1, m, tg.target().data_ptr(),
+                                               stride_b, abi.RT_BANDS_FRAME, ts.cuda_stream)
                     elif not tg.idle:  # (the compositor rank only assembles)
                         ctx.render_bands_batch(W, H, rb.band_rows, band_rank, band_world, m, tg.target().data_ptr(),
                                                stride_b, out_fmt, ts.cuda_stream)
@@ -894,6 +968,12 @@ def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, s
         traffic = pmc["hbm_bytes_per_launch"] / pmc_frames * launch_frames if pmc else None
         valu_insts = (pmc.get("counters") or {}).get("SQ_INSTS_VALU") if pmc else None
         valu_frame = valu_insts / pmc_frames if valu_insts else None  # wave instructions per frame
+        r0_note = ""
+        if comp and tail:
+            r0_note = (f" (rank 0 renders the last {tail} rows and decodes, ranks 1..N-1 trace the {Hc} above: "
+                       f"measured share)")
+        elif comp:
+            r0_note = " (compositor: rank 0 decodes, ranks 1..N-1 trace)"
         brute_tops = (f_alg / steps / max(1, world - 1 if comp else world)) * launch_frames / kernel_s / 1e12
         out = {
             "metric": METRIC,
@@ -915,13 +995,14 @@ def dist_leg(args, config_name, rank, world, local, torch, dist, Context, abi, s
                 "width": W, "height": H, "spheres": len(sc.spheres), "planes": len(sc.planes),
                 "lights": len(sc.lights), "depth": sc.recursion_limit + 1,
                 "parallelism": f"interleaved {args.band_rows}-row bands x {world - 1 if comp else world} ranks + RCCL gather to "
-                f"rank 0{' (compositor: rank 0 decodes, ranks 1..N-1 trace)' if comp else ''}"
+                "rank 0" + r0_note
                 + (" [collectives: " + ("library RCCL on the trace stream" if (tg is not None and tg.coll is not None)
                                         else "torch.distributed") + "]")
                 + (" (one gather per frame)" if args.no_pipeline else
                    f" ({tg.F if tg is not None else args.batch} frames per gather, {args.band_format} bands, double-buffered: the gather of "
                    f"one batch overlaps the trace of the next)"),
                 "rays_per_frame": rays_per_frame,
+                "rank0_tail_rows": tail if comp else None,
             },
             "roofline": {
                 "bound": "hbm",

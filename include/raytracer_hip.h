@@ -191,6 +191,11 @@ int rt_set_scene(rt_ctx* ctx,
 
 /* ---- camera (mirrors RayTracer.cs:511-523, :543-554, :892-896, :1058-1061) ---- */
 int rt_set_camera(rt_ctx* ctx, const rt_camera* camera);
+/* (ABI 9) The view's height: later renders of a width x height frame with height <= view_height trace
+ * rows [0, height) of the view of a width x view_height frame (TracePixel's y / height, :963-965, with
+ * the view's height) -- the multi-GPU pipeline's tracing ranks when rank 0 renders the frame's last rows
+ * itself; 0 (the default) = each render's own height.  The debug view ignores it. */
+int rt_set_view_height(rt_ctx* ctx, int view_height);
 int rt_get_camera(const rt_ctx* ctx, rt_camera* camera);
 int rt_camera_view(const rt_camera* camera, int width, int height, rt_view* out_view);
 int rt_camera_on_key(rt_camera* camera, int key);

@@ -157,7 +157,7 @@ def run_batched(rank, world, port, cfg, width, height, band_rows, frames, per_ba
 
 
 def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batch, result_path, rank0_codec=False,
-              compositor=False, speculate=0, spec_after_drain=False):
+              compositor=False, speculate=0, spec_after_drain=False, tail=0):
     """bench.py's default N>1 step: F frames per batch, tile-encoded band sets (host mirror of
     rt_encode_bands), size all_reduce + gather, rank 0 decodes every frame (host mirror of
     rt_decode_gathered) and checks it against the oracle."""
@@ -182,14 +182,16 @@ def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batc
             sc.camera = ((0.0, 0.0, 0.0), 0.04 * k - 0.1, -0.02 * k)
             return sc
 
-        # compositor: ranks 1..N-1 are band ranks 0..N-2 of a band world of N-1, rank 0 only decodes
+        # compositor: ranks 1..N-1 are band ranks 0..N-2 of a band world of N-1, rank 0 only decodes;
+        # with `tail` rows, ranks 1..N-1 cover rows [0, H - tail) and rank 0 renders the last `tail` rows
         brank, bworld = (max(0, rank - 1), world - 1) if compositor else (rank, world)
-        rb = RowBands(width, height, band_rows, brank, bworld)
+        hb = height - tail  # the band geometry's rows
+        rb = RowBands(width, hb, band_rows, brank, bworld)
         got = {}
         pending = {}  # batch -> (frame ring, frames) decoded, not yet read out of its ring
 
         def encode(raw, n, wire, size, _stream):
-            b = tilecodec.encode(raw.numpy()[:n * rb.slot_elems], width, height, band_rows, brank, bworld, n)
+            b = tilecodec.encode(raw.numpy()[:n * rb.slot_elems], width, hb, band_rows, brank, bworld, n)
             wire.numpy()[:len(b)] = np.frombuffer(b, dtype=np.uint8)
             size[0] = len(b)
 
@@ -198,8 +200,8 @@ def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batc
             # so a batch's frames are read out of the ring only before the ring is rendered again)
             host = recv.numpy()
             fr = frames_.numpy().reshape(-1, height, width)
-            for r in range(first_rank, bworld):
-                tilecodec.decode_into(fr[:n], host[r * rank_stride:(r + 1) * rank_stride], width, height,
+            for r in range(first_rank, bworld):  # (rows [0, hb) of each frame)
+                tilecodec.decode_into(fr[:n, :hb], host[r * rank_stride:(r + 1) * rank_stride], width, hb,
                                       band_rows, r, bworld)
             pending[g.decode_batch] = (fr, n)
 
@@ -210,9 +212,9 @@ def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batc
                     got[b * g.F + f] = fr[f].copy()
                     fr[f] = -7  # the ring slot is reused: stale pixels must not pass
 
-        g = TileBandGather(rb, "cpu", per_batch, lambda n: tilecodec.layout(width, height, band_rows, bworld, n),
+        g = TileBandGather(rb, "cpu", per_batch, lambda n: tilecodec.layout(width, hb, band_rows, bworld, n),
                            encode, decode, rank0_codec=rank0_codec, compositor=compositor, phys_rank=rank,
-                           phys_world=world)
+                           phys_world=world, tail_rows=tail)
         if rank == 0:
             for ring in g.frames:
                 ring.fill_(-7)
@@ -228,7 +230,11 @@ def run_tiles(rank, world, port, cfg, width, height, band_rows, frames, per_batc
                 g.commit()
                 continue
             dst = g.target().numpy()
-            if g.direct:  # rank 0 renders its bands into their frame rows
+            if g.direct and tail:  # rank 0 renders the frame's last `tail` rows into its frame
+                dst = dst.reshape(height, width)
+                rows, _ = pyoracle.render(scene_for(k), pyoracle.MODE_NEAREST, 2, rows=(hb, height))
+                dst[hb:height] = rows
+            elif g.direct:  # rank 0 renders its bands into their frame rows
                 dst = dst.reshape(height, width)
                 for l0, y0, n in rb.row_spans():
                     rows, _ = pyoracle.render(scene_for(k), pyoracle.MODE_NEAREST, 2, rows=(y0, y0 + n))

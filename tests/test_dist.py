@@ -138,7 +138,7 @@ def test_scatter_gathered_host_matches_scatter_host():
                           # warm-up drained the pipeline (speculative gather-first path)
                           (8, 5, 5, False, True, 1.25, True)])
 def test_gloo_tile_encoded_gather(tmp_path, world, frames, per_batch, rank0_codec, compositor, speculate,
-                                  after_drain):
+                                  after_drain, tail=0):
     """bench.py's default N>1 step: tile-encoded band sets, size all_reduce + gather, three-stage
     pipeline; every frame decodes to its own oracle frame, the last batch may be partial.  With
     `compositor` (bench.py at N >= 8) rank 0 traces nothing and decodes every band set.  With
@@ -154,7 +154,7 @@ def test_gloo_tile_encoded_gather(tmp_path, world, frames, per_batch, rank0_code
     result = tmp_path / "result.txt"
     procs = [ctx.Process(target=dist_worker.run_tiles,
                          args=(r, world, port, "C3", 43, 29, 4, frames, per_batch, str(result), rank0_codec,
-                               compositor, speculate, after_drain))
+                               compositor, speculate, after_drain, tail))
              for r in range(world)]
     for p in procs:
         p.start()
@@ -166,6 +166,18 @@ def test_gloo_tile_encoded_gather(tmp_path, world, frames, per_batch, rank0_code
             p.kill()
     assert codes == [0] * world, codes
     assert result.read_text() == "ok"
+
+
+@pytest.mark.parametrize("world,frames,per_batch,tail,speculate,after_drain",
+                         [(2, 5, 2, 8, 0, False), (3, 7, 3, 4, 0, False), (4, 5, 2, 12, 0, False),
+                          (8, 5, 5, 4, 1.25, True), (3, 9, 2, 8, 0.5, True), (4, 7, 7, 24, 1.25, True)])
+def test_gloo_tile_gather_rank0_tail(tmp_path, world, frames, per_batch, tail, speculate, after_drain):
+    """Rank 0's measured share (bench.py rank0_tail_rows): ranks 1..N-1 trace rows [0, H - tail) as a band
+    world of N-1 and tile-encode them; rank 0 renders the last `tail` rows straight into its frames and
+    decodes the others' -- every frame (29 rows: the band geometry's rows are cut at 29 - tail, not a
+    multiple of the 8-row tile) equals the oracle's, including the driver's N = 8 one-batch speculative
+    shape and a forced second gather (margin 0.5)."""
+    test_gloo_tile_encoded_gather(tmp_path, world, frames, per_batch, False, True, speculate, after_drain, tail)
 
 
 def test_deferred_size_check_decision():
@@ -190,6 +202,12 @@ def test_deferred_size_check_decision():
     assert g.pending_checks == [] and g.max_per_frame == 808 / 4
     with pytest.raises(RuntimeError):
         g.ring_of(1)
+    # a deferred run longer than three batches: batch 3's encode would overwrite batch 0's size slot
+    g.pending_checks = [(0, 4, 800, 0)]
+    g.batch = 3
+    with pytest.raises(RuntimeError, match="deferred size check"):
+        g._stage_a(None, 4)
+    assert g.batch == 3
 
 
 def test_world_of_one_direct_rank_exchanges_nothing(monkeypatch):

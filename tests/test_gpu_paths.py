@@ -139,13 +139,16 @@ def test_tile_pipeline_on_cuda_streams(extra, shape):
     assert line["verified_frames"] >= 16 and line["n_gpus"] == 1
 
 
-@pytest.mark.parametrize("world,extra", [(2, ["--compositor", "auto"]), (3, ["--compositor", "on"])])
+@pytest.mark.parametrize("world,extra", [(2, []), (3, ["--rank0-share", "off", "--compositor", "on"]),
+                                         (3, ["--rank0-share", "48"]), (4, ["--rank0-share", "auto"])])
 def test_bench_multi_rank_rehearsal(world, extra):
     """bench.py --gpus N as N processes (started by bench.py itself through torch.distributed.run)
     sharing this GPU, collectives over gloo (--rehearse-gloo: RCCL refuses two ranks on one GPU):
     every rank's N > 1 code path -- its bands, the tile codec, the pipelined size reduce and
-    gather, rank 0's decode (or compositor mode), the barrier and max-over-ranks timing -- with
-    rank 0's frames checked against a single-launch render (--verify)."""
+    gather, rank 0's decode (or compositor mode, or rank 0's measured share: the frame's last rows
+    rendered by rank 0, the rows above traced by ranks 1..N-1 with the whole frame's view), the
+    barrier and max-over-ranks timing -- with rank 0's frames checked against a single-launch render
+    (--verify)."""
     env = dict(os.environ)
     for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT"):
         env.pop(k, None)

@@ -55,9 +55,13 @@ def main():
         buf = np.zeros((1 << 20, 4), dtype=np.uint32)
         assert lib.rt_debug_wave_times(buf.ctypes.data, buf.nbytes) == 0
         r = buf[:n]
-        start = r[:, 0].astype(np.int64) | (r[:, 1].astype(np.int64) << 32)
+        start = r[:, 0].astype(np.int64)  # RTC low 32 bits: unwrap (a launch lasts far less than 2^31 ticks)
+        if start.max() - start.min() > (1 << 31):
+            start = np.where(start < (1 << 31), start + (1 << 32), start)
         start -= start.min()
         dur = r[:, 2].astype(np.int64)
+        cyc = r[:, 1].astype(np.int64)  # shader-clock cycles of the wave (s_memtime)
+        mhz = cyc / np.maximum(dur, 1) * 100.0  # RTC ticks at 100 MHz
         end = start + dur
         span = end.max()
         hw, xcc = r[:, 3] & 0xFFFFFF, r[:, 3] >> 24
@@ -71,9 +75,10 @@ def main():
                          start100=start.max() * TICK_US, end10=pct(end, 10) * TICK_US, end50=pct(end, 50) * TICK_US,
                          end90=pct(end, 90) * TICK_US, end99=pct(end, 99) * TICK_US, dur50=pct(dur, 50) * TICK_US,
                          dur99=pct(dur, 99) * TICK_US, durmax=dur.max() * TICK_US, cus=ncu, idle_tail=idle_tail * TICK_US,
-                         work=float(dur.sum()) * TICK_US))
+                         work=float(dur.sum()) * TICK_US,
+                         mhz=float(np.sum(cyc) / max(np.sum(dur), 1) * 100.0)))
         if rep == a.reps - 1 and a.save:
-            np.savez(a.save, start=start * TICK_US, dur=dur * TICK_US, tiles_x=tx, tiles_y=ty)
+            np.savez(a.save, start=start * TICK_US, dur=dur * TICK_US, cyc=cyc, tiles_x=tx, tiles_y=ty)
         if rep == a.reps - 1:
             order = np.argsort(-end)[:12]
             print(f"# {a.config} {W}x{H} batch={a.batch}: {n} waves on {ncu} CUs; the 12 last to finish "
@@ -86,6 +91,19 @@ def main():
             edges = np.arange(0, span + step, step)
             res = [(int(((start <= t) & (end > t)).sum())) for t in edges]
             print(f"# resident waves per {step // 100} us:", " ".join(str(x) for x in res))
+            # shader clock seen by the waves (cycles / RTC time), per frame and per 100 us of start time
+            per = tx * ty
+            for f in range(a.batch):
+                sl = slice(f * per, (f + 1) * per)
+                print(f"# frame {f}: wave-us {dur[sl].sum() * TICK_US:.0f}, clock {cyc[sl].sum() / max(dur[sl].sum(), 1) * 100:.0f} MHz, "
+                      f"cycles {cyc[sl].sum() / 1e6:.1f} M")
+            bucket = 10000  # 100 us
+            line = []
+            for b0 in range(0, int(span) + 1, bucket):
+                k = (start >= b0) & (start < b0 + bucket)
+                if k.sum() > 100:
+                    line.append(f"{b0 // 100}:{cyc[k].sum() / max(dur[k].sum(), 1) * 100:.0f}")
+            print("# clock (MHz) of the waves starting in each 100 us:", " ".join(line))
             if a.map:
                 d = dur[: tx * ty].reshape(ty, tx).astype(float) * TICK_US
                 by, bx = max(1, ty // 34), max(1, tx // 60)

@@ -225,7 +225,8 @@ struct rt_ctx {
     // of LaunchParams they gave (per-sphere screen boxes: a few us of host trig per launch)
     bool view_ok = false;
     rt_camera view_cam{};
-    int view_w = 0, view_h = 0;
+    int view_w = 0, view_h = 0, view_rows = 0;
+    int view_height = 0;  // rt_set_view_height: the view's height (0: each render's own frame height)
     LaunchParams view_lp{};
 };
 
@@ -486,21 +487,24 @@ void copy_view(const LaunchParams& from, LaunchParams& to) {
     std::memcpy(to.row_order, from.row_order, sizeof(uint16_t) * (size_t)from.row_order_n);
 }
 
+// The view of a W x VH frame (VH: rt_set_view_height, else H), of which a render traces rows [0, H).
 int view_params(rt_ctx* ctx, int W, int H, LaunchParams& lp) {
-    if (ctx->view_ok && ctx->view_w == W && ctx->view_h == H &&
+    const int VH = ctx->view_height > 0 ? ctx->view_height : H;
+    if (H > VH) return fail(ctx, RT_ERR_INVALID_ARG, "frame height %d above the view height %d", H, VH);
+    if (ctx->view_ok && ctx->view_w == W && ctx->view_h == VH && ctx->view_rows == H &&
         std::memcmp(&ctx->view_cam, &ctx->cam, sizeof ctx->cam) == 0) {
         copy_view(ctx->view_lp, lp);
         return RT_OK;
     }
     rt_view v;
-    int rc = rt_camera_view(&ctx->cam, W, H, &v);
-    if (rc != RT_OK) return fail(ctx, rc, "invalid frame size %dx%d", W, H);
+    int rc = rt_camera_view(&ctx->cam, W, VH, &v);
+    if (rc != RT_OK) return fail(ctx, rc, "invalid frame size %dx%d", W, VH);
     lp.cam[0] = v.position.x, lp.cam[1] = v.position.y, lp.cam[2] = v.position.z;
     lp.right[0] = v.right.x, lp.right[1] = v.right.y, lp.right[2] = v.right.z;
     lp.up[0] = v.up.x, lp.up[1] = v.up.y, lp.up[2] = v.up.z;
     lp.fwd[0] = v.forward.x, lp.fwd[1] = v.forward.y, lp.fwd[2] = v.forward.z;
     lp.pw = v.plane_width, lp.ph = v.plane_height, lp.nearc = v.near_clip;
-    lp.W = W, lp.H = H;
+    lp.W = W, lp.H = VH;  // (the screen boxes and the row order in the view's pixels)
     // primary-segment sphere constants (origin = camera for every pixel)
     const std::vector<DevSphere>& sph = ctx->layout.host_sph;
     lp.prim_const = sph.size() <= (size_t)MAX_PRIM_CONST ? 1 : 0;
@@ -511,8 +515,9 @@ int view_params(rt_ctx* ctx, int W, int H, LaunchParams& lp) {
             lp.pbox[i] = prim_box(lp, sph[i]);
         }
     lp.row_order_n = row_order(lp, ctx->layout, lp.row_order);  // dispatch-order candidate 0 (order_pick)
+    lp.H = H;  // the rows traced (validity, band counts); a cut view's row order no longer matches: not lone
     copy_view(lp, ctx->view_lp);
-    ctx->view_cam = ctx->cam, ctx->view_w = W, ctx->view_h = H, ctx->view_ok = true;
+    ctx->view_cam = ctx->cam, ctx->view_w = W, ctx->view_h = VH, ctx->view_rows = H, ctx->view_ok = true;
     return RT_OK;
 }
 
@@ -539,21 +544,22 @@ void scene_params(const rt_ctx* ctx, const Device& d, LaunchParams& lp) {
 // Rebuilt only when the frame size or view-plane size changes; frames in flight may read
 // the old table, so the device is synchronised first.
 int view_tables(rt_ctx* ctx, Device& d, LaunchParams& lp) {
-    if (d.tab_w != lp.W || d.tab_h != lp.H || d.tab_pw != lp.pw || d.tab_ph != lp.ph || !d.d_view_tab) {
-        std::vector<float> t((size_t)lp.W + (size_t)lp.H);
+    const int VH = ctx->view_height > 0 ? ctx->view_height : lp.H;  // the view's height (ly of row y)
+    if (d.tab_w != lp.W || d.tab_h != VH || d.tab_pw != lp.pw || d.tab_ph != lp.ph || !d.d_view_tab) {
+        std::vector<float> t((size_t)lp.W + (size_t)VH);
         for (int x = 0; x < lp.W; ++x) {
             const float px = (float)x / (float)lp.W - 0.5f;
             t[(size_t)x] = px * lp.pw;
         }
-        for (int y = 0; y < lp.H; ++y) {
-            const float py = (float)y / (float)lp.H - 0.5f;
+        for (int y = 0; y < VH; ++y) {
+            const float py = (float)y / (float)VH - 0.5f;
             t[(size_t)lp.W + (size_t)y] = py * lp.ph;
         }
         HIP_TRY(ctx, hipDeviceSynchronize());
         int rc = grow(ctx, (void**)&d.d_view_tab, &d.view_tab_cap, t.size() * sizeof(float));
         if (rc != RT_OK) return rc;
         HIP_TRY(ctx, hipMemcpy(d.d_view_tab, t.data(), t.size() * sizeof(float), hipMemcpyHostToDevice));
-        d.tab_w = lp.W, d.tab_h = lp.H, d.tab_pw = lp.pw, d.tab_ph = lp.ph;
+        d.tab_w = lp.W, d.tab_h = VH, d.tab_pw = lp.pw, d.tab_ph = lp.ph;
     }
     lp.lxt = d.d_view_tab;
     lp.lyt = d.d_view_tab + lp.W;
@@ -1278,6 +1284,12 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
     ctx->has_scene = true;
     ctx->view_ok = false;
     ctx->scene_gen++;
+    return RT_OK;
+}
+
+int rt_set_view_height(rt_ctx* ctx, int view_height) {
+    if (!ctx || view_height < 0) return fail(ctx, RT_ERR_INVALID_ARG, "rt_set_view_height: bad arguments");
+    ctx->view_height = view_height;
     return RT_OK;
 }
 

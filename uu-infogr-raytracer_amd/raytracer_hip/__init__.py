@@ -118,6 +118,10 @@ class Context:
     def set_camera(self, camera: abi.rt_camera):
         self._check(self.lib.rt_set_camera(self.ptr, C.byref(camera)))
 
+    def set_view_height(self, view_height: int):
+        """Later renders of a W x H frame trace rows [0, H) of a W x view_height view (0: H itself)."""
+        self._check(self.lib.rt_set_view_height(self.ptr, int(view_height)))
+
     def get_camera(self) -> abi.rt_camera:
         c = abi.rt_camera()
         self._check(self.lib.rt_get_camera(self.ptr, C.byref(c)))

@@ -114,6 +114,7 @@ EXPORTS = [
     ("rt_set_scene", C.c_int, [C.c_void_p, C.POINTER(rt_sphere), C.c_int, C.POINTER(rt_plane), C.c_int,
                                C.POINTER(rt_light), C.c_int, rt_vec3, C.c_int]),
     ("rt_set_camera", C.c_int, [C.c_void_p, C.POINTER(rt_camera)]),
+    ("rt_set_view_height", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_get_camera", C.c_int, [C.c_void_p, C.POINTER(rt_camera)]),
     ("rt_camera_view", C.c_int, [C.POINTER(rt_camera), C.c_int, C.c_int, C.POINTER(rt_view)]),
     ("rt_camera_on_key", C.c_int, [C.POINTER(rt_camera), C.c_int]),

@@ -279,10 +279,18 @@ class TileBandGather:
     1080p frame (≈3 µs) plus the decode of the other 7/8 (≈2 µs) made it the slowest rank;
     without the trace the slowest rank traces and encodes 1/7.  Rank 0 still
     takes part in both collectives (size 0; its own gather slot is receive slot N-1, scratch).
+
+    Rank 0's measured share (`tail_rows` > 0, with the compositor geometry): ranks 1..N-1 trace rows
+    [0, H') of the frame (H' = H - tail_rows; `rb` is the band geometry of that H'-row frame, traced
+    with the full frame's view: rt_set_view_height) and rank 0 renders the frame's last tail_rows rows
+    itself, straight into its frames (whole bands: tail_rows a multiple of band_rows), beside decoding
+    the others' -- a share sized so that its trace plus the decode take as long as the others' trace
+    (bench.py rank0_tail_rows; tail_rows 0 is the compositor).  `frame_h` = H.
     """
 
     def __init__(self, rb: RowBands, device, frames_per_batch, layout_fn, encode, decode, rank0_codec=False,
-                 compositor=False, phys_rank=None, phys_world=None, fused=False, coll=None, main_stream=None):
+                 compositor=False, phys_rank=None, phys_world=None, fused=False, coll=None, main_stream=None,
+                 tail_rows=0):
         import torch
         self.rb, self.F, self.device = rb, max(1, frames_per_batch), torch.device(device)
         self.cuda = self.device.type == "cuda"
@@ -294,10 +302,14 @@ class TileBandGather:
             raise ValueError("compositor mode: the band world is N-1 and band rank = rank-1")
         if not self.compositor and (self.pworld != rb.world or self.prank != rb.rank):
             raise ValueError("band geometry and process group differ outside compositor mode")
+        self.tail = int(tail_rows)
+        if self.tail and (not self.compositor or rank0_codec or self.tail % rb.band_rows):
+            raise ValueError("rank 0's tail rows: compositor geometry, whole bands, rank 0 outside the codec")
         self.root = self.prank == 0
         self.first_rank = 0 if (rank0_codec or self.compositor) else 1
-        self.direct = self.root and not rank0_codec and not self.compositor  # rank 0 renders into its frames
-        self.idle = self.root and self.compositor  # rank 0 only assembles
+        # rank 0 renders into its frames: its interleaved bands, or its tail rows
+        self.direct = self.root and ((not rank0_codec and not self.compositor) or self.tail > 0)
+        self.idle = self.root and self.compositor and not self.tail  # rank 0 only assembles
         # a world of one rank that renders straight into its frames has nothing to exchange: no size
         # reduce, gather or decode is issued (the one-GPU rehearsal of the default path then measures
         # the trace and the pipeline's bookkeeping alone)
@@ -316,7 +328,8 @@ class TileBandGather:
         # physical rank r's receive slot: r (compositor: its band rank r-1; rank 0's own: slot N-1)
         self.recv = ([torch.zeros(self.pworld * self.rank_stride, dtype=torch.uint8, device=self.device)
                       for _ in range(2)] if self.root else [None, None])
-        self.frame_elems = rb.width * rb.height
+        self.frame_h = rb.height + self.tail  # (the frame's rows: the band geometry's and rank 0's tail)
+        self.frame_elems = rb.width * self.frame_h
         self.frames = ([torch.zeros(self.F * self.frame_elems, dtype=torch.int32, device=self.device)
                         for _ in range(3)] if self.root else None)
         # coll (GPUs): the library's collectives (LibraryCollectives) issued on `main_stream`, the
@@ -479,6 +492,10 @@ class TileBandGather:
             self._stage_b()
         while self.stage_c and self.stage_c[0][0] <= b - 3:
             self._stage_c()
+        for pb, _, _, _ in self.pending_checks:
+            if b - pb >= 3:  # this encode would overwrite size/wire slot i before pb's deferred check read it
+                raise RuntimeError(f"batch {b}: batch {pb}'s deferred size check is still pending "
+                                   f"(defer_checks allows runs of at most three batches; call check_deferred)")
         # an empty pipeline (a run's first batch; all of a short run): speculative gather first
         first = self.capacity_per_frame is not None and not self.stage_b and not self.stage_c
         if b - 3 in self.gathered_ev:  # wire i was last read by gather b-3
@@ -562,7 +579,9 @@ class TileBandGather:
         (defer_checks) -- each batch's size reduce is issued here, outside the caller's region.  Returns
         True when every speculative gather sufficed (the batches are final); False when some wire
         outgrew its gather (every rank sees the same reduced size, so every rank returns the same) --
-        those batches stay provisional and the run must be repeated without speculation."""
+        those batches move to `abandoned` (ring_of refuses them for good: their ring slots are reused by
+        later batches) and the run must be repeated without speculation.  A deferred run spans at most
+        three batches: _stage_a raises before a fourth batch would overwrite a pending check's size slot."""
         ok = True
         for b, n_frames, n_spec, i in self.pending_checks:
             # the wire sizes' maximum over ranks (collective: every rank checks alike), then read back
