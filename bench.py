@@ -605,43 +605,57 @@ def auto_batch_frames(ctx, W, H, rb, band_rank, band_world, idle, steps, torch, 
 DECODE_S_PER_PX = 1.1e-12
 
 
+def solve_rank0_tail(T, D, H, band_rows, world, probe):
+    """rank0_tail_rows' model: T = s per whole frame's trace, D = s per whole frame's decode, probe(rows) = s per
+    frame of the last `rows` rows.  Solves t(h) + D (H - h) / H = (T - t(h)) / (N - 1) with t(h) ~ c h, c measured at
+    the uniform share and then once more at the solution.  Returns (h in whole bands, the uniform share hu, c);
+    h >= hu means rank 0 stays interleaved, 0 the compositor."""
+    hu = max(band_rows, (H // world) // band_rows * band_rows)  # the uniform share, whole bands
+    h, c = float(hu), probe(hu) / hu
+    for _ in range(2):  # the linear model, then once more with the slope measured at its solution
+        denom = c * world / (world - 1) - D / H
+        h = (T / (world - 1) - D) / denom if denom > 0 else 0.0
+        hb = int(h // band_rows) * band_rows
+        if hb <= 0 or hb >= hu:
+            break
+        c = probe(hb) / hb
+    return int(max(0.0, h) // band_rows) * band_rows, hu, c
+
+
 def rank0_tail_rows(ctx, W, H, band_rows, world, rank, torch, dist, log=None):
     """Rank 0's share of an N > 1 leg (every rank takes part and gets the same answer): -1 = rank 0 is an
     ordinary band rank (interleaved 1/N), 0 = compositor (rank 0 only decodes), h > 0 = rank 0 renders
     the frame's last h rows (whole bands) itself and ranks 1..N-1 the rows above them.  Rank 0 measures
-    the full frame's trace T and the trace of a candidate tail t(h) (two-frame launches after a warm one)
+    the full frame's trace T and the trace of a candidate tail t(h) (4-frame launches, HIP events, best of 3
+    after a warm one, every rank idle)
     and solves  t(h) + D (H - h) / H = (T - t(h)) / (N - 1)  for h with t(h) ~ c h (c from the probe,
     refined once at the solution), D = the decode of a whole frame (DECODE_S_PER_PX).  A
     solution at or above the uniform share 1/N keeps rank 0 interleaved."""
-    import time as _t
     from raytracer_hip import abi as _abi
     ans = torch.tensor([-1.0], dtype=torch.float64, device="cuda")
+    # every rank idle first: on a shared-GPU rehearsal another rank's set-up work would land in rank 0's probe
+    torch.cuda.synchronize()
+    dist.barrier() if world > 1 else None
     if rank == 0:
-        buf = torch.empty(2 * W * H, dtype=torch.int32, device="cuda")
-        st = torch.cuda.current_stream().cuda_stream
+        frames = 4
+        buf = torch.empty(frames * W * H, dtype=torch.int32, device="cuda")
+        st = torch.cuda.current_stream()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 
-        def probe(rows):  # two frames of the last `rows` rows (rows = H: the whole frame)
-            t = 0.0
-            for _ in range(2):
-                torch.cuda.synchronize()
-                t0 = _t.perf_counter()
-                ctx.render_bands_batch(W, H, band_rows, (H - rows) // band_rows, 1, 2, buf.data_ptr(), W * H * 4,
-                                       _abi.RT_BANDS_FRAME, st)
-                torch.cuda.synchronize()
-                t = (_t.perf_counter() - t0) / 2
-            return t
+        def probe(rows):  # s per frame of the last `rows` rows (rows = H: the whole frame): best of 3 after a warm one
+            best = float("inf")
+            for k in range(4):
+                e0.record(st)
+                ctx.render_bands_batch(W, H, band_rows, (H - rows) // band_rows, 1, frames, buf.data_ptr(), W * H * 4,
+                                       _abi.RT_BANDS_FRAME, st.cuda_stream)
+                e1.record(st)
+                e1.synchronize()
+                if k:
+                    best = min(best, e0.elapsed_time(e1) * 1e-3 / frames)
+            return best
         T = probe(H)
         D = DECODE_S_PER_PX * W * H
-        hu = max(band_rows, (H // world) // band_rows * band_rows)  # the uniform share, whole bands
-        h, c = float(hu), probe(hu) / hu
-        for _ in range(2):  # the linear model, then once more with the slope measured at its solution
-            denom = c * world / (world - 1) - D / H
-            h = (T / (world - 1) - D) / denom if denom > 0 else 0.0
-            hb = int(h // band_rows) * band_rows
-            if hb <= 0 or hb >= hu:
-                break
-            c = probe(hb) / hb
-        hb = int(max(0.0, h) // band_rows) * band_rows
+        hb, hu, c = solve_rank0_tail(T, D, H, band_rows, world, probe)
         ans[0] = -1.0 if hb >= hu else float(hb)
         if log:
             log(f"rank 0 share: T {T * 1e6:.1f} us/frame, decode {D * 1e6:.1f} us/frame, tail slope "

@@ -80,3 +80,27 @@ def test_cpu_baseline_reports_its_spread():
 def test_percentiles_nearest_rank():
     assert bench.percentiles([5, 1, 2, 3, 4]) == [1, 3, 5]
     assert bench.percentiles([7]) == [7, 7, 7]
+
+
+def test_rank0_tail_solver():
+    """bench.solve_rank0_tail (rank 0's measured share): with a uniform cost per row it reproduces the
+    closed form h/H = (T/(N-1) - D) / (N T/(N-1) - D), floored to whole bands; rows that cost more than the average
+    shrink the tail; a decode above the others' trace share makes rank 0 the compositor (0 rows); a solution at or
+    above the uniform share keeps it interleaved (h >= hu)."""
+    T, D, H, br = 1136e-6, 36.5e-6, 4320, 8
+    for n in (2, 4, 8):
+        calls = []
+
+        def probe(rows):
+            calls.append(rows)
+            return T * rows / H
+        h, hu, c = bench.solve_rank0_tail(T, D, H, br, n, probe)
+        x = (T / (n - 1) - D) / (n * T / (n - 1) - D)
+        assert h == int(x * H // br) * br and h % br == 0 and 0 < h < hu, (n, h, x * H)
+        assert hu == (H // n) // br * br and calls[0] == hu and abs(c - T / H) < 1e-15
+    h_uniform = bench.solve_rank0_tail(T, D, H, br, 8, lambda rows: T * rows / H)[0]
+    h_costly = bench.solve_rank0_tail(T, D, H, br, 8, lambda rows: 1.5 * T * rows / H)[0]
+    assert h_costly < h_uniform
+    assert bench.solve_rank0_tail(10e-6, 20e-6, 1080, br, 2, lambda rows: 10e-6 * rows / 1080)[0] == 0
+    h, hu, _ = bench.solve_rank0_tail(T, 0.0, H, br, 4, lambda rows: 0.5 * T * rows / H)  # a cheap tail, no decode
+    assert h >= hu

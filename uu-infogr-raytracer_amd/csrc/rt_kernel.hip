@@ -1297,7 +1297,10 @@ __device__ __forceinline__ unsigned shadow_members_grid(const LaunchParams& p, f
     return memb;
 }
 
-template <typename T>
+// A2OK: every light of the scene has 2a = 2 p.p finite and > 0 (LaunchParams::lights_a2_ok, host-checked; the
+// kernel instantiation MERGED == 2): no per-light uniform check and no literal-formula fallback in the loop
+// (C4 -0.4 %, C5 -0.4 %, profiles/ab/r05_merged_loop_ab.txt).
+template <bool A2OK, typename T>
 __device__ __forceinline__ unsigned shadow_merged(const LaunchParams& p, unsigned memb, f3 hp, unsigned want, bool diff,
                                                   bool act, T& tl) {
     unsigned long long U = __builtin_amdgcn_ballot_w64(memb != 0u);
@@ -1320,7 +1323,7 @@ __device__ __forceinline__ unsigned shadow_merged(const LaunchParams& p, unsigne
             const float b = 2.0f * dot(oc, mk(l.px, l.py, l.pz));
             const float disc = b * b - l.a4 * c;
             bool hit = false;
-            if (l.a2 > 0.0f && l.a2 < __builtin_inff()) {  // wave-uniform (shadow_blocked<.., THRESH>)
+            if (A2OK || (l.a2 > 0.0f && l.a2 < __builtin_inff())) {  // wave-uniform (shadow_blocked<.., THRESH>)
                 if (__builtin_amdgcn_ballot_w64(sphere_candidate(b, disc)) != 0) {
                     const float sq = cr_sqrt(disc);
                     hit = -b - sq >= l.sh_t;
@@ -1343,7 +1346,7 @@ __device__ __forceinline__ unsigned shadow_merged(const LaunchParams& p, unsigne
 // the deeper segment `sec`), then each light in order, then ambient.  Inactive lanes
 // return `sec` unchanged.  Shadow rays (IntersectShadowLight :573-582) of the lanes that
 // need them form one bundle per light (common direction = the light position).
-template <bool GPOW, bool MERGED, typename T>
+template <bool GPOW, int MERGED, typename T>
 __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool is_sphere, int prim, f3 hp, f3 d, float t,
                                            f3 sec, unsigned* n_shadow, T& tl, int level) {
     // idle lanes (act false) carry a copy of an active lane's record: same branches, result dropped
@@ -1357,7 +1360,7 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
     // cost more than the tests it saved, profiles/ab/r03_shadow_merged.txt).
     // MERGED (an instantiation of its own, so that neither path's code and registers burden the
     // other: S <= 64, 1 <= L <= SHADOW_MERGE_L, chosen on the host)
-    const bool merged = MERGED && __builtin_amdgcn_ballot_w64(diff) != 0;
+    const bool merged = MERGED != 0 && __builtin_amdgcn_ballot_w64(diff) != 0;
     unsigned blk = 0u;
     if (merged)
         for (int li = 0; li < p.L; ++li) tl.shadow(diff);  // (diagnostic tally of the rays resolved)
@@ -1378,7 +1381,7 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
         } else {
             memb = shadow_members_fast(p, make_shadow_sphere(hp, diff), want);
         }
-        blk = shadow_merged(p, memb, hp, want, diff, act, tl);
+        blk = shadow_merged<MERGED == 2>(p, memb, hp, want, diff, act, tl);
     }
     f3 normal;
     float tile = 1.0f;
@@ -1401,7 +1404,7 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
         const float att = is_sphere ? cr_rcp(t) * t : (float)(1.0 / ((double)t * (double)t));
         const f3 kd = mk(m.kd[0], m.kd[1], m.kd[2]);
         ShadowSphere SS{};
-        if (!MERGED) SS = make_shadow_sphere(hp, diff);  // one bound for every light's shadow rays
+        if (MERGED == 0) SS = make_shadow_sphere(hp, diff);  // one bound for every light's shadow rays
         unsigned long long umask = 0;  // (diagnostic builds: the union of the lights' candidates)
         for (int li = 0; li < p.L; ++li) {
             const DevLight& l = p.li[li];
@@ -1419,7 +1422,7 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
             ph = add(ph, spec);
             const bool need = diff && shadow_matters(ph, l.intensity, att);
             bool blocked = merged ? ((blk >> li) & 1u) != 0 : !need;
-            if (!MERGED && __builtin_amdgcn_ballot_w64(need) != 0) {  // some lane's pixel depends on this test
+            if (MERGED == 0 && __builtin_amdgcn_ballot_w64(need) != 0) {  // some lane's pixel depends on this test
                 // (MERGED without a diffuse lane: no lane needs a test)
                 tl.shadow(need);
                 const f3 hs = need ? hp : SS.O;  // idle lanes mirror a shading lane (results ignored)
@@ -1468,7 +1471,7 @@ __device__ __forceinline__ f3 shade_bundle(const LaunchParams& p, bool act, bool
 // Backward fold (converged call, all 64 lanes): level by level from the deepest, every recorded
 // hit is shaded; a mirror hit consumes the colour of the segment after it (levels 0..limit push
 // at most one record each, so K = limit + 1 records suffice).  Returns the lane's colour.
-template <bool GPOW, bool MERGED, typename STK, typename T>
+template <bool GPOW, int MERGED, typename STK, typename T>
 __device__ __forceinline__ f3 fold_converged(const LaunchParams& p, STK& stk, f3 leaf, unsigned* cnt, T& tl) {
     f3 col = leaf;
     const int depth = stk.n;
@@ -1500,7 +1503,7 @@ __device__ __forceinline__ f3 fold_converged(const LaunchParams& p, STK& stk, f3
 
 // BUNDLE kernel (scenes with >= CULL_MIN_SPHERES spheres): converged control flow so that
 // every segment and every light can form a wave bundle and cull the sphere list.
-template <int K, bool GPOW, bool TILES, bool MERGED, typename T>
+template <int K, bool GPOW, bool TILES, int MERGED, typename T>
 __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int tile_x, float2* stk_lv, float* stk_dv,
                                                       T& tl) {
     const int lane = threadIdx.x & 63;
@@ -1590,7 +1593,7 @@ __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int
 // spilled to VGPR lanes) and 64 VGPRs (8 waves): C4 -2.6 %, C5 -7.5 %.  Not with GPOW (the f64
 // Math.Pow path would spill ~150 B/lane to scratch).  The direct kernel needs no cap (79 SGPRs, 48
 // VGPRs).
-template <int K, bool GPOW, bool STATS, bool TILES, bool MERGED>
+template <int K, bool GPOW, bool STATS, bool TILES, int MERGED>
 __device__ __forceinline__ void bundle_kernel_body(const LaunchParams& p) {
     constexpr int LDS_LEVELS = StackFor<K>::lds_levels;  // LdsStack slots, else unused
     __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
@@ -1604,12 +1607,12 @@ __device__ __forceinline__ void bundle_kernel_body(const LaunchParams& p) {
     const unsigned cnt = trace_tile_bundle<K, GPOW, TILES, MERGED>(p, blockIdx.x, stk_lv, stk_dv, tl);
     add_counters<STATS>(p, threadIdx.x & 63, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
 }
-template <int K, bool STATS, bool TILES, bool MERGED>
+template <int K, bool STATS, bool TILES, int MERGED>
 __global__ __launch_bounds__(WG_THREADS, 8) __attribute__((amdgpu_num_sgpr(80))) void trace_bundle_kernel(
     LaunchParams p) {
     bundle_kernel_body<K, false, STATS, TILES, MERGED>(p);
 }
-template <int K, bool STATS, bool TILES, bool MERGED>
+template <int K, bool STATS, bool TILES, int MERGED>
 __global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel_gpow(LaunchParams p) {
     bundle_kernel_body<K, true, STATS, TILES, MERGED>(p);
 }
@@ -1734,7 +1737,7 @@ struct DirectK {
 };
 // tiles of a tile row per workgroup for single-frame launches (8: +2.5 % on C2, profiles/r04_final_check.txt)
 constexpr int SINGLE_WPG = 4;
-template <bool GPOW, bool STATS, bool TILES, bool MERGED>
+template <bool GPOW, bool STATS, bool TILES, int MERGED>
 struct BundleK {
     template <int K>
     struct at {
@@ -1750,10 +1753,12 @@ template <bool GPOW, bool STATS, bool TILES = false>
 static void launch_variant(const LaunchParams& p, bool bundle, dim3 grid, dim3 block, hipStream_t s) {
     if (bundle) {
         // the merged shadow pass's instantiation for S <= 64 spheres and 1..SHADOW_MERGE_L lights
-        if (p.S <= 64 && p.L >= 1 && p.L <= SHADOW_MERGE_L)
-            launch_by_depth<BundleK<GPOW, STATS, TILES, true>::template at>(p, grid, block, s);
+        if (p.S <= 64 && p.L >= 1 && p.L <= SHADOW_MERGE_L && p.lights_a2_ok)
+            launch_by_depth<BundleK<GPOW, STATS, TILES, 2>::template at>(p, grid, block, s);
+        else if (p.S <= 64 && p.L >= 1 && p.L <= SHADOW_MERGE_L)
+            launch_by_depth<BundleK<GPOW, STATS, TILES, 1>::template at>(p, grid, block, s);
         else
-            launch_by_depth<BundleK<GPOW, STATS, TILES, false>::template at>(p, grid, block, s);
+            launch_by_depth<BundleK<GPOW, STATS, TILES, 0>::template at>(p, grid, block, s);
     }
     else if (SINGLE_WPG > 1 && !STATS && !TILES && p.n_frames <= 1 && p.copy_z == 0) {
         // a lone frame: SINGLE_WPG tiles of a tile row per workgroup
