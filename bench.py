@@ -396,8 +396,11 @@ def tick_rates(ctx, W, H, torch, n=20, reps=3, n_single=200):
     - tick_async_fps_incl_d2h: rt_render_async into two alternating registered buffers and an
       rt_wait per pair (a display loop two frames deep);
     - tick_async_deep_fps_incl_d2h: n frames queued into n registered buffers, one rt_wait.
-    rt_render_async's D2H of frame k rides in frame k+1's launch (copy slice) or rt_wait's."""
+    rt_render_async's D2H of frame k rides in frame k+1's launch (copy slice) or rt_wait's.
+    Every shape runs with the work counters off (rt_set_counting(0), what the plugin's display loop sets:
+    the reference's Tick counts nothing); they are on again on return."""
     import numpy as np
+    ctx.set_counting(False)
 
     def med(fn, frames=n):
         fn()  # warm
@@ -443,9 +446,11 @@ def tick_rates(ctx, W, H, torch, n=20, reps=3, n_single=200):
         out[key], out[key + "_runs"] = med(fn)
     for hb in hosts:
         ctx.unregister_host(hb)
+    ctx.set_counting(True)
     out["tick_note"] = (f"median of {reps} runs each; single_launch_fps = rt_render_device one frame per launch into "
                         f"HBM, runs of {n_single} frames (single_launch_fps_20: runs of {n}); tick_* runs of {n} "
-                        f"frames, including the D2H into registered host memory (PCIe)")
+                        f"frames, including the D2H into registered host memory (PCIe); work counters off "
+                        f"(rt_set_counting(0), the display loop's setting)")
     return out
 
 
@@ -457,6 +462,7 @@ def plugin_ticks(ctx, configs, scenes, n=20, reps=3):
     each hand their own bands over their own link)."""
     import numpy as np
     out = {}
+    ctx.set_counting(False)  # the display loop's setting (the plugin shim's), as tick_rates
     for name in configs:
         sc = scenes.config(name)
         W, H = sc.width, sc.height
@@ -490,6 +496,7 @@ def plugin_ticks(ctx, configs, scenes, n=20, reps=3):
         for b in bufs:
             ctx.unregister_host(b)
         out[sc.name] = e
+    ctx.set_counting(True)
     return out
 
 
@@ -1226,9 +1233,10 @@ def main_single(args, torch, Context, abi, scenes):
         if tick_cfgs:
             out["tick_by_config"] = plugin_ticks(ctx, tick_cfgs, scenes)
             out["tick_by_config"]["note"] = ("plugin-path Tick() per config, one GPU: tick_fps = rt_render (synchronous, "
-                                             "large frames in chunks whose PCIe copy rides in the next chunk's trace), "
-                                             "tick_async_fps = rt_render_async two frames deep; d2h_gbs = frame bytes "
-                                             "x fps; median of 3 runs of 20 frames")
+                                             "large frames traced in chunks, each chunk's PCIe copy by the copy engine "
+                                             "on a second stream under the next chunk's trace), tick_async_fps = "
+                                             "rt_render_async two frames deep; d2h_gbs = frame bytes x fps; median of 3 "
+                                             "runs of 20 frames; work counters off (the display loop's setting)")
             ctx.set_scene(sc)
     also = [c for c in (x.strip() for x in args.also.split(",")) if c and c.upper() != sc.name.upper()]
     if also:

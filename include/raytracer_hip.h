@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define RT_ABI_VERSION 9
+#define RT_ABI_VERSION 10
 
 /* ---- status codes ---------------------------------------------------------- */
 enum {
@@ -372,7 +372,7 @@ int rt_debug_segments(rt_ctx* ctx, int width, int height, int sample_stride, rt_
 /* Device timing of trace launches, copies and gathers with HIP event pairs: every
  * `every`-th operation of each kind is timed (the first one always), 0 = none.  Default 64:
  * an event pair costs several microseconds of GPU time, 17 % of a 1080p frame if every
- * frame were timed.  Counters (rays) are always exact. */
+ * frame were timed.  Counters (rays) are always exact (for the launches that count, rt_set_counting). */
 int rt_set_timing(rt_ctx* ctx, int every);
 /* Dispatch order of single-frame launches (rt_render, rt_render_device on scenes with fewer than
  * 12 spheres): the order in which the kernel's tiles start, which sets a lone frame's tail.  The
@@ -383,6 +383,13 @@ int rt_set_timing(rt_ctx* ctx, int every);
 int rt_dispatch_order(rt_ctx* ctx, int* out_order);
 int rt_get_stats(rt_ctx* ctx, rt_stats* out_stats);
 int rt_reset_stats(rt_ctx* ctx);
+/* ABI 10.  on = 1 (the default): every trace launch adds its rays to the counters above (frame 0 of a
+ * batch launch counts for all its frames; one device atomic pair per wave).  on = 0: the kernels count
+ * nothing -- the display loop's setting, since the reference's Tick counts nothing and in a one-frame
+ * launch every wave's atomics cost the frame 8-13 % (1080p; 4 % at 4K).  Launches made with counting
+ * off still add to frames, pixels and launches, not to primary_rays (= the pixels of counted launches)
+ * nor to the other ray and test counts.  Returns RT_ERR_INVALID_ARG unless on is 0 or 1. */
+int rt_set_counting(rt_ctx* ctx, int on);
 /* Traces one width x height frame of the current camera with the diagnostic kernels (same
  * pixels, plus executed-work tallies) into a context-owned buffer and returns its work.
  * Synchronous; single-GPU contexts; does not touch rt_get_stats' counters. */

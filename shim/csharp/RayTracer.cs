@@ -43,6 +43,7 @@ internal static class Native {
                                                                  [Out] Segment[] segments, int capacity, out int count);
     [DllImport(Lib)] internal static extern int rt_set_timing(IntPtr ctx, int every);
     [DllImport(Lib)] internal static extern int rt_dispatch_order(IntPtr ctx, out int order);
+    [DllImport(Lib)] internal static extern int rt_set_counting(IntPtr ctx, int on);  // ABI 10
 
     internal static void Check(int rc, IntPtr ctx) {
         if (rc != 0) throw new InvalidOperationException($"libraytracer_hip error {rc}: {Marshal.PtrToStringAnsi(rt_last_error(ctx))}");
@@ -59,6 +60,8 @@ internal sealed class RayTracer : IDisposable {
         this.screen = screen;
         int nGpus = int.TryParse(Environment.GetEnvironmentVariable("RT_GPUS"), out int g) ? g : 1;
         Native.Check(Native.rt_create(nGpus, out _ctx), IntPtr.Zero);
+        // the reference's Tick counts no rays: the display loop runs without the library's work counters
+        Native.Check(Native.rt_set_counting(_ctx, 0), _ctx);
         // the hard-coded scene of RayTracer.cs:441-469
         static Native.Vec3 V(float x, float y, float z) => new(x, y, z);
         static Native.Material M(Native.Vec3 kd, Native.Vec3 ka, Native.Vec3 ks, float n, Native.Vec3 km) =>

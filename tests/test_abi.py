@@ -57,8 +57,8 @@ def test_struct_layouts_match_header():
 
 
 def test_abi_version(rtlib):
-    # 9: the per-worker Tick hand-off, RT_CREATE_SHARED_DEVICE (8: rt_comm_probe; 7: rt_comm_* collectives)
-    assert rtlib.rt_abi_version() == 9 == abi.RT_ABI_VERSION
+    # 10: rt_set_counting (9: the per-worker Tick hand-off, RT_CREATE_SHARED_DEVICE; 8: rt_comm_probe; 7: rt_comm_*)
+    assert rtlib.rt_abi_version() == 10 == abi.RT_ABI_VERSION
     hdr = open(HEADER).read()
     assert re.search(r"#define RT_ABI_VERSION (\d+)", hdr).group(1) == str(abi.RT_ABI_VERSION)
     assert re.search(r"RT_CREATE_RCCL_GATHER = (\d+), RT_CREATE_SHARED_DEVICE = (\d+)", hdr).groups() == \

@@ -354,6 +354,41 @@ def test_stats_accumulate_and_reset(gpu_ctx, golden):
     assert gpu_ctx.stats()["primary_rays"] == 0
 
 
+@pytest.mark.parametrize("cid", ["C2", "C4"])
+def test_counting_off_same_pixels_no_rays(gpu_ctx, golden, cid):
+    """rt_set_counting (ABI 10): with counting off a launch writes the same pixels (golden CRC, one-frame and
+    4-frame batch launches, direct and bundle kernels) and adds frames / pixels / launches but no rays; on again,
+    the counts resume exactly (the golden per-frame counts).  Only 0 and 1 are accepted."""
+    e = golden["cases"][cid]
+    sc = scenes.config(cid)
+    W, H = sc.width, sc.height
+    gpu_ctx.set_scene(sc)
+    gpu_ctx.reset_stats()
+    gpu_ctx.set_counting(False)
+    try:
+        assert crc(gpu_ctx.render(W, H)) == e["crc32"]
+        import torch
+        big = torch.empty(4 * W * H, dtype=torch.int32, device="cuda")
+        st_ = torch.cuda.current_stream()
+        gpu_ctx.render_bands_batch(W, H, 8, 0, 1, 4, big.data_ptr(), W * H * 4, abi.RT_BANDS_FRAME, st_.cuda_stream)
+        torch.cuda.synchronize()
+        frames = big.cpu().numpy().reshape(4, H, W)
+        assert all(crc(f) == e["crc32"] for f in frames)
+        st = gpu_ctx.stats()
+        assert st["pixels"] == 5 * W * H and st["launches"] == 2
+        assert st["primary_rays"] == st["reflect_rays"] == st["shadow_rays"] == 0 and st["sphere_tests"] == 0
+    finally:
+        gpu_ctx.set_counting(True)
+    gpu_ctx.render(W, H)
+    gpu_ctx.render_bands_batch(W, H, 8, 0, 1, 4, big.data_ptr(), W * H * 4, abi.RT_BANDS_FRAME, st_.cuda_stream)
+    torch.cuda.synchronize()
+    st = gpu_ctx.stats()
+    want = {k: 5 * e["stats"][k] for k in ("primary_rays", "reflect_rays", "shadow_rays")}
+    assert ray_counts(st) == want and st["pixels"] == 10 * W * H
+    for bad in (2, -1):
+        assert gpu_ctx.lib.rt_set_counting(gpu_ctx.ptr, bad) == abi.RT_ERR_INVALID_ARG
+
+
 def test_sampled_timing(gpu_ctx):
     sc = scenes.config("C1").resized(320, 180)
     gpu_ctx.set_scene(sc)

@@ -22,6 +22,7 @@ def main():
     ap.add_argument("--lib", default="", help="library build to load instead of the in-tree one")
     ap.add_argument("--bands", default="", help="R/N: trace only rank R's 8-row bands of an N-rank world")
     ap.add_argument("--batch", type=int, default=1, help="frames per launch (rt_render_bands_batch)")
+    ap.add_argument("--no-count", action="store_true", help="rt_set_counting(0): the launches count no rays")
     a = ap.parse_args()
     import torch
     from raytracer_hip import Context, abi, scenes
@@ -36,6 +37,8 @@ def main():
     outs = [torch.empty(W * H, dtype=torch.int32, device="cuda") for _ in range(a.inflight)]
     ctx = Context(1)
     ctx.set_scene(sc)
+    if a.no_count:
+        ctx.set_counting(False)
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(a.inflight - 1)]
     sp = [s.cuda_stream for s in streams]
     ptrs = [o.data_ptr() for o in outs]
@@ -71,7 +74,7 @@ def main():
     st = ctx.stats()
     kern = st["kernel_ms"] / st["launches"] * 1e3 if st["kernel_ms"] else float("nan")
     order = ctx.dispatch_order() if hasattr(ctx, "dispatch_order") else None
-    print(f"{os.path.basename(a.lib) or 'in-tree'} {a.config} {W}x{H} strip={a.strip or '-'} bands={a.bands or '-'} batch={a.batch} inflight={a.inflight}: "
+    print(f"{os.path.basename(a.lib) or 'in-tree'} {a.config} {W}x{H} strip={a.strip or '-'} bands={a.bands or '-'} batch={a.batch} inflight={a.inflight}{' no-count' if a.no_count else ''}: "
           f"wall/frame min {min(res):.2f} us median {sorted(res)[len(res)//2]:.2f} us; host enqueue/frame {min(enq):.2f} us"
           + (f"; dispatch order {order}" if order is not None else ""))
 

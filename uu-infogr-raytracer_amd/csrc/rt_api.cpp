@@ -209,6 +209,7 @@ struct rt_ctx {
     double kernel_ms = 0, last_kernel_ms = 0, copy_ms = 0, gather_ms = 0;
     uint64_t timed[3] = {0, 0, 0};  // timed launches, copies, gathers
     int timing_every = 64;
+    bool counting = true;  // rt_set_counting: trace launches add to the ray counters
     uint64_t scene_gen = 0;  // rt_set_scene calls (the dispatch-order measurements belong to one scene)
     int order_fixed = -1;    // RT_DISPATCH_ORDER=0/1/2: that candidate for every single-frame launch
     int32_t* host_staging = nullptr;
@@ -535,7 +536,7 @@ void scene_params(const rt_ctx* ctx, const Device& d, LaunchParams& lp) {
     lp.shslab = L.has_shg ? (const unsigned long long*)(base + L.off_shslab) : nullptr;
     lp.S = L.S, lp.P = L.P, lp.L = L.L, lp.limit = L.limit;
     lp.lights_a2_ok = L.lights_a2_ok ? 1 : 0;
-    lp.counters = d.d_counters;
+    lp.counters = ctx->counting ? d.d_counters : nullptr;  // nullptr: the kernels count nothing (rt_set_counting)
 }
 
 // Per-column / per-row view-plane coordinates of TracePixel (:963-965), computed with the
@@ -708,7 +709,7 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
     d.stream = saved;
     if (e != hipSuccess) return fail(ctx, RT_ERR_HIP, "trace launch failed: %s", hipGetErrorString((hipError_t)e));
     ctx->launches++;
-    for (int k = 0; k < nb; ++k) {  // pixels of rows < H in the launched bands
+    for (int k = 0; k < nb && ctx->counting; ++k) {  // pixels of rows < H in the launched bands (counted launches)
         const long long y0 = (long long)(first + k * step) * band_rows;
         ctx->prim_rays += (uint64_t)std::min<long long>(band_rows, (long long)H - y0) * (uint64_t)W * (uint64_t)n_frames;
     }
@@ -2078,6 +2079,12 @@ int rt_set_timing(rt_ctx* ctx, int every) {
     if (every < 0) return fail(ctx, RT_ERR_INVALID_ARG, "rt_set_timing: every must be >= 0");
     ctx->timing_every = every;
     for (Device& d : ctx->dev) d.op_count[0] = d.op_count[1] = d.op_count[2] = 0;
+    return RT_OK;
+}
+
+int rt_set_counting(rt_ctx* ctx, int on) {
+    if (!ctx || (on != 0 && on != 1)) return fail(ctx, RT_ERR_INVALID_ARG, "rt_set_counting: bad arguments");
+    ctx->counting = on != 0;
     return RT_OK;
 }
 

@@ -495,11 +495,16 @@ struct Tally<true, SMAX> {
 // host.  Every frame of a batch launch (grid z) traces the same view with the same
 // LaunchParams, so its counts are identical: frame 0 counts for all n_frames of them -- one
 // atomic pair per wave per launch instead of per frame (each device-scope atomic is a memory
-// round trip on MI355X, 32 B of HBM write traffic).
+// round trip on MI355X, 32 B of HBM write traffic).  In a one-frame launch every wave counts, and
+// the atomics cost the frame more than their round trips: C2 19.6 -> 22.5 us, C3 36.1 -> 39.6 us,
+// C4 337 -> 352 us per lone frame (+15 % L2 requests, +22 % waves parked on memory; spreading them
+// over 8192 slots instead of 256 changed nothing, profiles/r05_bundle_lone.txt) -- so a
+// display loop that never reads rt_get_stats turns them off (rt_set_counting, ABI 10).
 template <bool ST, int SM>
 __device__ __forceinline__ void add_counters(const LaunchParams& p, int lane, unsigned n_refl, unsigned n_shadow,
                                              const Tally<ST, SM>& tl) {
-    if (blockIdx.z != (unsigned)p.copy_z) return;  // wave-uniform: the first frame (behind a copy slice)
+    // wave-uniform: the first frame (behind a copy slice) counts, and only when the context counts at all
+    if (blockIdx.z != (unsigned)p.copy_z || p.counters == nullptr) return;
     const unsigned long long nf = p.n_frames > 1 ? (unsigned long long)p.n_frames : 1ull;
     const unsigned b = wave_count(n_refl), c = wave_count(n_shadow);
     const unsigned slot = (blockIdx.y * gridDim.x + blockIdx.x) % COUNTER_SLOTS;

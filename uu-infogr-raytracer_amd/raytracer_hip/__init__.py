@@ -122,6 +122,11 @@ class Context:
         """Later renders of a W x H frame trace rows [0, H) of a W x view_height view (0: H itself)."""
         self._check(self.lib.rt_set_view_height(self.ptr, int(view_height)))
 
+    def set_counting(self, on: bool):
+        """rt_set_counting (ABI 10): False = the trace launches count no rays (a display loop's setting; the
+        pixels are the same), True = every launch adds its rays to stats() (the default)."""
+        self._check(self.lib.rt_set_counting(self.ptr, 1 if on else 0))
+
     def get_camera(self) -> abi.rt_camera:
         c = abi.rt_camera()
         self._check(self.lib.rt_get_camera(self.ptr, C.byref(c)))

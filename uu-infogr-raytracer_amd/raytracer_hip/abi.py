@@ -14,7 +14,7 @@ PKG_ROOT = os.path.dirname(_HERE)
 # RAYTRACER_HIP_LIB selects another build of the library (A/B variants under lib/ab/)
 LIB_PATH = os.environ.get("RAYTRACER_HIP_LIB") or os.path.join(PKG_ROOT, "lib", "libraytracer_hip.so")
 
-RT_ABI_VERSION = 9  # include/raytracer_hip.h
+RT_ABI_VERSION = 10  # include/raytracer_hip.h
 RT_COMM_ID_BYTES = 128
 RT_CREATE_RCCL_GATHER = 1
 RT_CREATE_SHARED_DEVICE = 2
@@ -115,6 +115,7 @@ EXPORTS = [
                                C.POINTER(rt_light), C.c_int, rt_vec3, C.c_int]),
     ("rt_set_camera", C.c_int, [C.c_void_p, C.POINTER(rt_camera)]),
     ("rt_set_view_height", C.c_int, [C.c_void_p, C.c_int]),
+    ("rt_set_counting", C.c_int, [C.c_void_p, C.c_int]),
     ("rt_get_camera", C.c_int, [C.c_void_p, C.POINTER(rt_camera)]),
     ("rt_camera_view", C.c_int, [C.POINTER(rt_camera), C.c_int, C.c_int, C.POINTER(rt_view)]),
     ("rt_camera_on_key", C.c_int, [C.POINTER(rt_camera), C.c_int]),
