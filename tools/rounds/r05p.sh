@@ -12,4 +12,4 @@ for c in ${CFGS:-C3 C2 C4 C5}; do
      gpurun_out/trace_${c}_kernel_stats.csv $O/ 2>/dev/null
 done
 cp gpurun_out/pmc_traffic.json $O/
-tail -3 $O/trace_*_reconcile.txt
+for f in $O/trace_*_reconcile.txt; do tail -n 2 $f; done
