@@ -377,9 +377,10 @@ int rt_set_timing(rt_ctx* ctx, int every);
 /* Dispatch order of single-frame launches (rt_render, rt_render_device on scenes with fewer than
  * 12 spheres): the order in which the kernel's tiles start, which sets a lone frame's tail.  The
  * first launches of a scene and frame size time each candidate (0 tile rows by decreasing estimated
- * cost, 1 rows bottom to top, 2 rows varying fastest) and keep the fastest; the pixels are the same
+ * cost, 1 rows bottom to top, 2 rows varying fastest, 3 every tile by decreasing measured duration --
+ * the round's first launch records each tile's duration) and keep the fastest; the pixels are the same
  * under every order.  *out_order: the candidate in use, -1 while still measuring (ABI 8 addition;
- * RT_DISPATCH_ORDER=0/1/2 in the environment at rt_create fixes it). */
+ * RT_DISPATCH_ORDER=0/1/2/3 in the environment at rt_create fixes it). */
 int rt_dispatch_order(rt_ctx* ctx, int* out_order);
 int rt_get_stats(rt_ctx* ctx, rt_stats* out_stats);
 int rt_reset_stats(rt_ctx* ctx);

@@ -243,12 +243,13 @@ def test_render_device_on_torch_stream(gpu_ctx, golden):
     assert crc(out.cpu().numpy()) == e["crc32"]
 
 
-@pytest.mark.parametrize("order", [0, 1, 2])
+@pytest.mark.parametrize("order", [0, 1, 2, 3])
 @pytest.mark.parametrize("cid", ["C1", "C2", "C3", "REF_1280x720"])
 def test_single_frame_dispatch_orders(golden, monkeypatch, cid, order):
-    """Each single-frame dispatch order (rows by estimated cost, bottom to top, rows varying fastest:
-    rt_dispatch_order's candidates, fixed through RT_DISPATCH_ORDER) renders the golden frame, through
-    rt_render and rt_render_device."""
+    """Each single-frame dispatch order (rows by estimated cost, bottom to top, rows varying fastest, every
+    tile by measured duration: rt_dispatch_order's candidates, fixed through RT_DISPATCH_ORDER) renders the
+    golden frame, through rt_render and rt_render_device (order 3: the first launch records the tile
+    durations, the later ones run the sorted order)."""
     import torch
     monkeypatch.setenv("RT_DISPATCH_ORDER", str(order))
     e = golden["cases"][cid]
@@ -257,11 +258,36 @@ def test_single_frame_dispatch_orders(golden, monkeypatch, cid, order):
     try:
         ctx.set_scene(sc)
         assert ctx.dispatch_order() == order
-        assert crc(ctx.render(sc.width, sc.height)) == e["crc32"]
+        for _ in range(2):
+            assert crc(ctx.render(sc.width, sc.height)) == e["crc32"]
         out = torch.zeros(sc.width * sc.height, dtype=torch.int32, device="cuda")
-        ctx.render_device(sc.width, sc.height, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
-        torch.cuda.synchronize()
-        assert crc(out.cpu().numpy()) == e["crc32"]
+        for _ in range(2):
+            out.zero_()
+            ctx.render_device(sc.width, sc.height, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+            torch.cuda.synchronize()
+            assert crc(out.cpu().numpy()) == e["crc32"]
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("size", [(203, 117), (8, 8), (9, 300), (1000, 9)])
+def test_measured_tile_order_ragged_vs_oracle(oracle, monkeypatch, size):
+    """The measured tile order (candidate 3) on frames whose tile count is not a multiple of the 4-tile
+    workgroup and whose edge tiles are partial: the padded entries trace nothing, every pixel = the oracle's,
+    on the recording launch and on the sorted ones; a size change records again."""
+    monkeypatch.setenv("RT_DISPATCH_ORDER", "3")
+    sc = scenes.config("C3").resized(*size)
+    want, _ = oracle.render(sc, oracle.MODE_NEAREST, 4)
+    ctx = Context(1)
+    try:
+        ctx.set_scene(sc)
+        for _ in range(3):
+            assert_same(ctx.render(sc.width, sc.height).copy(), want, f"C3 {size}")
+        sc2 = scenes.config("C3").resized(size[1], size[0])
+        want2, _ = oracle.render(sc2, oracle.MODE_NEAREST, 4)
+        ctx.set_scene(sc2)
+        for _ in range(2):
+            assert_same(ctx.render(sc2.width, sc2.height).copy(), want2, f"C3 {size[::-1]}")
     finally:
         ctx.close()
 
@@ -285,7 +311,7 @@ def test_dispatch_order_measured_then_kept(golden):
                 if k % 10 == 9:
                     torch.cuda.synchronize()
             torch.cuda.synchronize()
-            assert ctx.dispatch_order() in (0, 1, 2)
+            assert ctx.dispatch_order() in (0, 1, 2, 3)
             for o in outs:
                 assert crc(o.cpu().numpy()) == e["crc32"]
     finally:

@@ -168,7 +168,17 @@ struct Device {
         int W = 0, H = 0;          // frame size and scene generation the measurements belong to
         uint64_t scene_gen = 0, gen = 0;
         uint64_t since = 0;        // single-frame launches since the choice (re-measured every ORDER_RETUNE)
-        std::vector<float> ms[3];
+        std::vector<float> ms[4];
+        // candidate 3: the tiles in decreasing order of their measured duration (the first single-frame
+        // launch of a measuring round records every tile's duration; tile_order_prepare)
+        struct Tiles {
+            int W = 0, H = 0;
+            uint64_t gen = 0, scene_gen = 0;
+            bool recorded = false, built = false;
+            uint32_t* d_order = nullptr;  // padded to SINGLE_WPG (ty = 0xffff past the last tile)
+            uint32_t* d_cost = nullptr;   // RTC ticks per tile
+            size_t order_cap = 0, cost_cap = 0;
+        } tiles;
         struct Probe {
             hipEvent_t a = nullptr, b = nullptr;
             int cand = 0;
@@ -576,8 +586,9 @@ int view_tables(rt_ctx* ctx, Device& d, LaunchParams& lp) {
 // bracketed by an event pair; once every candidate has ORDER_SAMPLES durations the one with the least
 // median is kept, and measured again after ORDER_RETUNE launches (the view drifts).  Candidates:
 // 0 tile rows by decreasing estimated cost (row_order), 1 tile rows bottom to top, 2 rows varying fastest
-// (column-major over the 4-tile workgroups), natural row order.
-constexpr int ORDER_CANDIDATES = 3, ORDER_SAMPLES = 7;
+// (column-major over the 4-tile workgroups), natural row order, 3 every tile by decreasing measured
+// duration (longest first: a lone frame's tail is its costliest waves started late).
+constexpr int ORDER_CANDIDATES = 4, ORDER_SAMPLES = 7;
 constexpr float ORDER_MARGIN = 1.01f;  // another order replaces candidate 0 only when > 1 % faster (median)
 constexpr uint64_t ORDER_RETUNE = 1u << 14;
 
@@ -648,6 +659,45 @@ bool order_begin(Device& d, int cand, hipStream_t s) {
 
 void order_end(Device& d, hipStream_t s) { (void)hipEventRecord(d.order.pending.back().b, s); }
 
+// Candidate 3 of a single-frame launch (the direct kernel's 4-tile workgroups): the first launch of each
+// measuring round (and of each frame size / scene) records every tile's duration instead of being timed as a
+// probe; the first candidate-3 launch after it reads the durations back (one stream synchronisation per
+// round) and uploads the tiles sorted by decreasing duration, ties in natural order.  Returns the candidate
+// to launch (candidate 3 falls back to 0 while its order is not ready).
+int tile_order_prepare(rt_ctx* ctx, Device& d, int W, int H, hipStream_t s, LaunchParams& lp, int cand, bool* probe) {
+    Device::OrderTuner::Tiles& o = d.order.tiles;
+    if (o.gen != d.order.gen || o.scene_gen != ctx->scene_gen || o.W != W || o.H != H) {
+        o.gen = d.order.gen, o.scene_gen = ctx->scene_gen, o.W = W, o.H = H;
+        o.recorded = o.built = false;
+    }
+    const size_t tx = (size_t)(W + 7) / 8, ty = (size_t)(H + 7) / 8, n = tx * ty;
+    const size_t padded = (n + SINGLE_WPG - 1) / SINGLE_WPG * SINGLE_WPG;
+    if (ty > 0xffff || tx > 0xffff) return cand == 3 ? 0 : cand;  // (not representable: candidates 0-2 only)
+    if (!o.recorded) {
+        int rc = grow(ctx, (void**)&o.d_cost, &o.cost_cap, n * sizeof(uint32_t));
+        if (rc == RT_OK) rc = grow(ctx, (void**)&o.d_order, &o.order_cap, padded * sizeof(uint32_t));
+        if (rc != RT_OK) return -1;
+        lp.tile_cost = o.d_cost;
+        o.recorded = true;
+        *probe = false;  // (the duration stores are not the candidate's own cost)
+        return cand == 3 ? 0 : cand;
+    }
+    if (cand == 3 && !o.built) {
+        std::vector<uint32_t> cost(n), order(padded, 0xffff0000u);
+        if (hipStreamSynchronize(s) != hipSuccess ||
+            hipMemcpy(cost.data(), o.d_cost, n * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+            return 0;
+        std::vector<uint32_t> idx(n);
+        for (size_t i = 0; i < n; ++i) idx[i] = (uint32_t)i;
+        std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+        for (size_t i = 0; i < n; ++i) order[i] = (uint32_t)((idx[i] / tx) << 16 | (idx[i] % tx));
+        if (hipMemcpy(o.d_order, order.data(), padded * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) return 0;
+        o.built = true;
+    }
+    if (cand == 3) lp.tile_order = o.d_order;
+    return cand;
+}
+
 // The fused encoder's target of a trace with out_fmt OUT_TILES (rt_render_bands_tiles).
 struct EncTarget {
     unsigned char* wire;
@@ -683,6 +733,9 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
     int cand = -1;
     if (lone) {
         cand = order_pick(ctx, d, W, H, &probe);
+        if (ctx->order_fixed < 0 ? d.order.chosen < 0 || cand == 3 : cand == 3)  // measuring, or the measured order
+            cand = tile_order_prepare(ctx, d, W, H, stream, lp, cand, &probe);
+        if (cand < 0) return fail(ctx, RT_ERR_OOM, "tile order buffers");
         if (cand == 1)
             for (int r = 0; r < lp.row_order_n; ++r) lp.row_order[r] = (uint16_t)(lp.row_order_n - 1 - r);
         if (cand == 2) lp.row_order_n = 0, lp.col_major = 1;
@@ -1009,6 +1062,8 @@ void rt_destroy(rt_ctx* ctx) {
         if (d.d_counters) (void)hipFree(d.d_counters);
         if (d.d_counters_diag) (void)hipFree(d.d_counters_diag);
         if (d.d_view_tab) (void)hipFree(d.d_view_tab);
+        if (d.order.tiles.d_order) (void)hipFree(d.order.tiles.d_order);
+        if (d.order.tiles.d_cost) (void)hipFree(d.order.tiles.d_cost);
         if (d.d_stage) (void)hipFree(d.d_stage);
         if (d.async_stream) (void)hipStreamDestroy(d.async_stream);
         if (d.stream) (void)hipStreamDestroy(d.stream);

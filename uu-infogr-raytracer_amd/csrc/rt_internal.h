@@ -191,7 +191,15 @@ struct LaunchParams {
     int row_order_n;
     int col_major;  // single-frame launches: tile rows vary fastest in dispatch order (grid x = rows)
     uint16_t row_order[ROW_ORDER_MAX];
+    // single-frame launches, measured order (order_pick candidate 3): dispatch position (workgroup x
+    // SINGLE_WPG + wave, a 1-D grid) -> tile (ty << 16 | tx; ty = 0xffff pads past the last tile), and
+    // tile_cost: when set, each wave stores its duration (RTC ticks) at tile ty * tiles_x + tx
+    const uint32_t* tile_order;
+    uint32_t* tile_cost;
 };
+// Tiles per workgroup of the direct kernel's single-frame launches (8: +2.5 % on C2,
+// profiles/r04_final_check.txt); the measured tile order (LaunchParams::tile_order) is padded to it.
+constexpr int SINGLE_WPG = 4;
 // The kernel argument block: raising ROW_ORDER_MAX or MAX_PRIM_CONST must not push it past 4 KiB.
 static_assert(sizeof(LaunchParams) < 4096, "LaunchParams is passed by value as the kernarg block (< 4 KiB)");
 

@@ -881,7 +881,11 @@ __device__ __forceinline__ unsigned trace_tile_direct(const LaunchParams& p, int
 // single-frame launches without a copy slice (fewer, larger workgroups: the dispatcher launches
 // one-wave groups no faster than ~6.9 us per 1080p frame, a floor a lone frame's launch pays in
 // full, tools/launch_probe.hip).  Each wave has its own LDS stack slice.
-template <int K, bool GPOW, bool STATS, int SMAX, bool TILES, int WPG = 1>
+// TORD (single-frame launches, WPG > 1): 0 = tile rows in row_order / col_major order, 1 = the measured tile
+// order (tile_order, a 1-D grid), 2 = as 0 and every wave records its duration (tile_cost).  Instantiations of
+// their own: the order read and the recording, compiled into the common kernel even when unused, cost a
+// one-frame launch 2 % and 10 % (C2 19.9 -> 20.3 / 22.4 us, profiles/ab/r05_tile_order.txt).
+template <int K, bool GPOW, bool STATS, int SMAX, bool TILES, int WPG = 1, int TORD = 0>
 __global__ __launch_bounds__(WG_THREADS * WPG) void trace_direct_kernel(LaunchParams p) {
     constexpr int LDS_LEVELS = StackFor<K>::lds_levels;  // LdsStack slots, else unused
     __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS * WPG : 1];
@@ -891,16 +895,40 @@ __global__ __launch_bounds__(WG_THREADS * WPG) void trace_direct_kernel(LaunchPa
         return;
     }
     Tally<STATS, SMAX> tl;
-    const int wave = WPG > 1 ? (int)(threadIdx.x >> 6) : 0;
+    const int wave = WPG > 1 && TORD != 0 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))
+                     : WPG > 1                ? (int)(threadIdx.x >> 6)
+                                              : 0;
     float2* lv = stk_lv + (LDS_LEVELS > 0 ? wave * LDS_LEVELS * WG_THREADS : 0);
     float* dv = stk_dv + (LDS_LEVELS > 0 ? wave * 3 * WG_THREADS : 0);
     // single-frame launches: tile rows in the host's cost order (LaunchParams::row_order), optionally
-    // with the rows varying fastest in dispatch order (col_major: grid x = tile rows)
+    // with the rows varying fastest in dispatch order (col_major: grid x = tile rows), or any tile order
+    // the host measured (tile_order: a 1-D grid, entry ty << 16 | tx)
     const bool cm = WPG > 1 && p.col_major;
     const int gx = cm ? (int)blockIdx.y : (int)blockIdx.x, gy = cm ? (int)blockIdx.x : (int)blockIdx.y;
-    const int tile_y = WPG > 1 && gy < p.row_order_n ? (int)p.row_order[gy] : gy;
-    const unsigned cnt = trace_tile_direct<K, GPOW, TILES>(p, gx * WPG + wave, tile_y, lv, dv, tl);
+    int tile_x = gx * WPG + wave, tile_y = WPG > 1 && gy < p.row_order_n ? (int)p.row_order[gy] : gy;
+    if constexpr (TORD == 1) {
+        const uint32_t t = p.tile_order[blockIdx.x * WPG + wave];
+        tile_x = (int)(t & 0xffffu), tile_y = (int)(t >> 16);  // (0xffff: past the frame, no pixel valid)
+    }
+    // the host measuring tile costs (order_pick): the wave's cost slot (null when not measuring) and start
+    // time wait in LDS -- nothing of it lives in registers across the trace (there it spilled: +9 VGPRs)
+    struct TileRec {
+        unsigned* slot;
+        unsigned t0;
+    };
+    __shared__ TileRec t_rec[TORD == 2 ? WPG : 1];
+    if (TORD == 2 && (threadIdx.x & 63) == 0) {
+        const unsigned tiles_x = (unsigned)(p.W + TILE_W - 1) / TILE_W, tiles_y = (unsigned)(p.H + TILE_H - 1) / TILE_H;
+        const bool in = p.tile_cost != nullptr && (unsigned)tile_x < tiles_x && (unsigned)tile_y < tiles_y;
+        t_rec[wave] = TileRec{in ? p.tile_cost + ((unsigned)tile_y * tiles_x + (unsigned)tile_x) : nullptr,
+                              in ? (unsigned)__builtin_amdgcn_s_memrealtime() : 0u};
+    }
+    const unsigned cnt = trace_tile_direct<K, GPOW, TILES>(p, tile_x, tile_y, lv, dv, tl);
     add_counters<STATS>(p, threadIdx.x & 63, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
+    if (TORD == 2 && (threadIdx.x & 63) == 0) {
+        const TileRec r = t_rec[threadIdx.x >> 6];
+        if (r.slot != nullptr) *r.slot = (unsigned)__builtin_amdgcn_s_memrealtime() - r.t0;
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -1733,15 +1761,13 @@ static void launch_by_depth(const LaunchParams& p, dim3 grid, dim3 block, hipStr
     else if (need <= 8) hipLaunchKernelGGL(KERNEL<8>::fn, grid, block, 0, s, p);
     else hipLaunchKernelGGL(KERNEL<64>::fn, grid, block, 0, s, p);
 }
-template <bool GPOW, bool STATS, int SMAX, bool TILES, int WPG = 1>
+template <bool GPOW, bool STATS, int SMAX, bool TILES, int WPG = 1, int TORD = 0>
 struct DirectK {
     template <int K>
     struct at {
-        static constexpr auto fn = trace_direct_kernel<K, GPOW, STATS, SMAX, TILES, WPG>;
+        static constexpr auto fn = trace_direct_kernel<K, GPOW, STATS, SMAX, TILES, WPG, TORD>;
     };
 };
-// tiles of a tile row per workgroup for single-frame launches (8: +2.5 % on C2, profiles/r04_final_check.txt)
-constexpr int SINGLE_WPG = 4;
 template <bool GPOW, bool STATS, bool TILES, int MERGED>
 struct BundleK {
     template <int K>
@@ -1768,8 +1794,18 @@ static void launch_variant(const LaunchParams& p, bool bundle, dim3 grid, dim3 b
     else if (SINGLE_WPG > 1 && !STATS && !TILES && p.n_frames <= 1 && p.copy_z == 0) {
         // a lone frame: SINGLE_WPG tiles of a tile row per workgroup
         const unsigned gxw = (grid.x + SINGLE_WPG - 1) / SINGLE_WPG;
-        const dim3 g(p.col_major ? grid.y : gxw, p.col_major ? gxw : grid.y, grid.z), b(WG_THREADS * SINGLE_WPG);
-        if (p.S <= DIRECT_SMAX)
+        const unsigned g1 = (grid.x * grid.y + SINGLE_WPG - 1) / SINGLE_WPG;  // tile_order: a 1-D grid
+        const dim3 g(p.tile_order ? g1 : p.col_major ? grid.y : gxw, p.tile_order ? 1u : p.col_major ? gxw : grid.y, grid.z),
+            b(WG_THREADS * SINGLE_WPG);
+        if (p.tile_cost != nullptr) {  // the host recording tile durations (natural / row / column order)
+            if (p.S <= DIRECT_SMAX)
+                launch_by_depth<DirectK<GPOW, false, DIRECT_SMAX, false, SINGLE_WPG, 2>::template at>(p, g, b, s);
+            else launch_by_depth<DirectK<GPOW, false, 0, false, SINGLE_WPG, 2>::template at>(p, g, b, s);
+        } else if (p.tile_order != nullptr) {
+            if (p.S <= DIRECT_SMAX)
+                launch_by_depth<DirectK<GPOW, false, DIRECT_SMAX, false, SINGLE_WPG, 1>::template at>(p, g, b, s);
+            else launch_by_depth<DirectK<GPOW, false, 0, false, SINGLE_WPG, 1>::template at>(p, g, b, s);
+        } else if (p.S <= DIRECT_SMAX)
             launch_by_depth<DirectK<GPOW, false, DIRECT_SMAX, false, SINGLE_WPG>::template at>(p, g, b, s);
         else launch_by_depth<DirectK<GPOW, false, 0, false, SINGLE_WPG>::template at>(p, g, b, s);
     } else if (p.S <= DIRECT_SMAX)
