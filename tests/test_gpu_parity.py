@@ -270,24 +270,61 @@ def test_single_frame_dispatch_orders(golden, monkeypatch, cid, order):
         ctx.close()
 
 
+@pytest.mark.parametrize("cid", ["C3", "C4"])
 @pytest.mark.parametrize("size", [(203, 117), (8, 8), (9, 300), (1000, 9)])
-def test_measured_tile_order_ragged_vs_oracle(oracle, monkeypatch, size):
+def test_measured_tile_order_ragged_vs_oracle(oracle, monkeypatch, size, cid):
     """The measured tile order (candidate 3) on frames whose tile count is not a multiple of the 4-tile
-    workgroup and whose edge tiles are partial: the padded entries trace nothing, every pixel = the oracle's,
-    on the recording launch and on the sorted ones; a size change records again."""
+    workgroup and whose edge tiles are partial -- the direct kernel (C3's scene) and the bundle kernel (C4's):
+    the padded entries trace nothing, every pixel = the oracle's, on the recording launch and on the sorted
+    ones; a size change records again."""
     monkeypatch.setenv("RT_DISPATCH_ORDER", "3")
-    sc = scenes.config("C3").resized(*size)
-    want, _ = oracle.render(sc, oracle.MODE_NEAREST, 4)
+    sc = scenes.config(cid).resized(*size)
+    want, _ = oracle.render(sc, oracle.MODE_NEAREST, 8)
     ctx = Context(1)
     try:
         ctx.set_scene(sc)
         for _ in range(3):
-            assert_same(ctx.render(sc.width, sc.height).copy(), want, f"C3 {size}")
-        sc2 = scenes.config("C3").resized(size[1], size[0])
-        want2, _ = oracle.render(sc2, oracle.MODE_NEAREST, 4)
+            assert_same(ctx.render(sc.width, sc.height).copy(), want, f"{cid} {size}")
+        sc2 = scenes.config(cid).resized(size[1], size[0])
+        want2, _ = oracle.render(sc2, oracle.MODE_NEAREST, 8)
         ctx.set_scene(sc2)
         for _ in range(2):
-            assert_same(ctx.render(sc2.width, sc2.height).copy(), want2, f"C3 {size[::-1]}")
+            assert_same(ctx.render(sc2.width, sc2.height).copy(), want2, f"{cid} {size[::-1]}")
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("order", [0, 3, None])
+@pytest.mark.parametrize("cid", ["C4", "C5"])
+def test_bundle_lone_frame_orders(golden, monkeypatch, cid, order):
+    """The bundle kernel's one-frame launches in natural order (0), in the measured tile order (3: the first
+    launch records the tile durations) and under the library's own choice: the golden frames, through
+    rt_render_device and rt_render."""
+    import torch
+    if order is None:
+        monkeypatch.delenv("RT_DISPATCH_ORDER", raising=False)
+    else:
+        monkeypatch.setenv("RT_DISPATCH_ORDER", str(order))
+    e = golden["cases"][cid]
+    sc = scenes.config(cid)
+    W, H = sc.width, sc.height
+    ctx = Context(1)
+    try:
+        ctx.set_scene(sc)
+        out = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+        st = torch.cuda.current_stream().cuda_stream
+        for k in range(60 if order is None else 3):  # (None: well past the tuner's 28 probes and its recording)
+            ctx.render_device(W, H, out.data_ptr(), st)
+            if k % 10 == 9 or order is not None:
+                torch.cuda.synchronize()
+                assert crc(out.cpu().numpy()) == e["crc32"]
+                out.zero_()
+        torch.cuda.synchronize()
+        if order is not None:
+            assert ctx.dispatch_order() == order
+        else:  # (1 and 2 launch the bundle kernel in natural order, like 0)
+            assert ctx.dispatch_order() in (0, 1, 2, 3)
+        assert crc(ctx.render(W, H)) == e["crc32"]
     finally:
         ctx.close()
 

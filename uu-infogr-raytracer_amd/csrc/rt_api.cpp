@@ -587,7 +587,10 @@ int view_tables(rt_ctx* ctx, Device& d, LaunchParams& lp) {
 // median is kept, and measured again after ORDER_RETUNE launches (the view drifts).  Candidates:
 // 0 tile rows by decreasing estimated cost (row_order), 1 tile rows bottom to top, 2 rows varying fastest
 // (column-major over the 4-tile workgroups), natural row order, 3 every tile by decreasing measured
-// duration (longest first: a lone frame's tail is its costliest waves started late).
+// duration (longest first: a lone frame's tail is its costliest waves started late; C3 36.3 -> 30.8 us,
+// profiles/ab/r05_tile_order.txt).  The bundle kernel's lone frames (its all-lights-ok merged
+// instantiation) take the same tuner: 0-2 are its natural order, 3 the measured one (C4 338 -> 302 us,
+// C5 1,136 -> 1,109 us -- faster than a frame of a 64-frame batch launch, 309 / 1,125 us).
 constexpr int ORDER_CANDIDATES = 4, ORDER_SAMPLES = 7;
 constexpr float ORDER_MARGIN = 1.01f;  // another order replaces candidate 0 only when > 1 % faster (median)
 constexpr uint64_t ORDER_RETUNE = 1u << 14;
@@ -727,20 +730,27 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
     lp.out_frame_bytes = frame_bytes;
     // single-frame launches of a whole frame on the direct kernel: the dispatch order (order_pick)
     const bool with_copy = slice && slice->words;
-    const bool lone = n_frames <= 1 && !enc && !with_copy && band_rows >= lp.local_rows &&
-                      lp.local_rows == H && lp.S < CULL_MIN_SPHERES && lp.row_order_n == (H + 7) / 8;
+    const bool whole = !enc && !with_copy && band_rows >= lp.local_rows && lp.local_rows == H;
+    const bool lone = n_frames <= 1 && whole && lp.S < CULL_MIN_SPHERES && lp.row_order_n == (H + 7) / 8;
+    // the bundle kernel's all-lights-ok merged instantiation (C4/C5): natural or measured tile order
+    const SceneLayout& L = ctx->layout;
+    const bool lone_bundle = n_frames <= 1 && whole && lp.S >= CULL_MIN_SPHERES && lp.S <= 64 && lp.L >= 1 &&
+                             lp.L <= SHADOW_MERGE_L && L.lights_a2_ok && !L.generic_pow;
     bool probe = false;
     int cand = -1;
-    if (lone) {
+    if (lone || lone_bundle) {
         cand = order_pick(ctx, d, W, H, &probe);
+        // (candidates 1 and 2 order the direct kernel's 4-tile groups: a bundle launch under them is natural order)
         if (ctx->order_fixed < 0 ? d.order.chosen < 0 || cand == 3 : cand == 3)  // measuring, or the measured order
             cand = tile_order_prepare(ctx, d, W, H, stream, lp, cand, &probe);
         if (cand < 0) return fail(ctx, RT_ERR_OOM, "tile order buffers");
-        if (cand == 1)
+        if (lone && cand == 1)
             for (int r = 0; r < lp.row_order_n; ++r) lp.row_order[r] = (uint16_t)(lp.row_order_n - 1 - r);
-        if (cand == 2) lp.row_order_n = 0, lp.col_major = 1;
+        if (lone && cand == 2) lp.row_order_n = 0, lp.col_major = 1;
+        if (lone_bundle) lp.row_order_n = 0;
     } else {
-        lp.row_order_n = 0;
+        lp.row_order_n = 0;  // (batch launches keep the natural order: the measured one measured no better,
+                             //  profiles/ab/r05_batch_tile_order_rejected.txt)
     }
     if (enc) {
         lp.out_fmt = OUT_TILES;

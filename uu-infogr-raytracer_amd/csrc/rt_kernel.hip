@@ -1537,10 +1537,10 @@ __device__ __forceinline__ f3 fold_converged(const LaunchParams& p, STK& stk, f3
 // BUNDLE kernel (scenes with >= CULL_MIN_SPHERES spheres): converged control flow so that
 // every segment and every light can form a wave bundle and cull the sphere list.
 template <int K, bool GPOW, bool TILES, int MERGED, typename T>
-__device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int tile_x, float2* stk_lv, float* stk_dv,
-                                                      T& tl) {
+__device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int tile_x, int tile_y, float2* stk_lv,
+                                                      float* stk_dv, T& tl) {
     const int lane = threadIdx.x & 63;
-    const TilePixel tpx = tile_pixel(p, tile_x * TILE_W + (lane & 7), blockIdx.y * TILE_H + (lane >> 3));
+    const TilePixel tpx = tile_pixel(p, tile_x * TILE_W + (lane & 7), tile_y * TILE_H + (lane >> 3));
     const int x = tpx.x, y = tpx.y;
     const bool valid = tpx.valid;
 
@@ -1614,7 +1614,7 @@ __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int
         // keeping x, r, y and `valid` live through the walk and the fold (64-VGPR cap: they were
         // the values spilled to scratch once the merged shadow pass raised the peak)
         const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
-        const TilePixel q = tile_pixel(p, tile_x * TILE_W + (ln & 7), blockIdx.y * TILE_H + (ln >> 3));
+        const TilePixel q = tile_pixel(p, tile_x * TILE_W + (ln & 7), tile_y * TILE_H + (ln >> 3));
         if (q.valid) store_pixel(p, q.r, q.y, q.x, px32);
     }
     return cnt;
@@ -1626,7 +1626,9 @@ __device__ __forceinline__ unsigned trace_tile_bundle(const LaunchParams& p, int
 // spilled to VGPR lanes) and 64 VGPRs (8 waves): C4 -2.6 %, C5 -7.5 %.  Not with GPOW (the f64
 // Math.Pow path would spill ~150 B/lane to scratch).  The direct kernel needs no cap (79 SGPRs, 48
 // VGPRs).
-template <int K, bool GPOW, bool STATS, bool TILES, int MERGED>
+// TORD: the single-frame launches' tile order as in the direct kernel (0 = natural, 1 = tile_order over the
+// 2-D grid, 2 = natural and every wave records its duration in tile_cost)
+template <int K, bool GPOW, bool STATS, bool TILES, int MERGED, int TORD = 0>
 __device__ __forceinline__ void bundle_kernel_body(const LaunchParams& p) {
     constexpr int LDS_LEVELS = StackFor<K>::lds_levels;  // LdsStack slots, else unused
     __shared__ float2 stk_lv[LDS_LEVELS > 0 ? LDS_LEVELS * WG_THREADS : 1];
@@ -1637,13 +1639,28 @@ __device__ __forceinline__ void bundle_kernel_body(const LaunchParams& p) {
     }
     Tally<STATS> tl;
     tl.init(p);
-    const unsigned cnt = trace_tile_bundle<K, GPOW, TILES, MERGED>(p, blockIdx.x, stk_lv, stk_dv, tl);
+    int tile_x = (int)blockIdx.x, tile_y = (int)blockIdx.y;
+    if constexpr (TORD == 1) {
+        const uint32_t t = p.tile_order[blockIdx.y * gridDim.x + blockIdx.x];
+        tile_x = (int)(t & 0xffffu), tile_y = (int)(t >> 16);  // (0xffff: past the frame, no pixel valid)
+    }
+    struct TileRec {
+        unsigned* slot;
+        unsigned t0;
+    };
+    __shared__ TileRec t_rec[1];
+    if (TORD == 2 && (threadIdx.x & 63) == 0)  // (a batch launch's frame 0 records; the others store nothing)
+        t_rec[0] = TileRec{blockIdx.z == (unsigned)p.copy_z ? p.tile_cost + (blockIdx.y * gridDim.x + blockIdx.x) : nullptr,
+                           (unsigned)__builtin_amdgcn_s_memrealtime()};
+    const unsigned cnt = trace_tile_bundle<K, GPOW, TILES, MERGED>(p, tile_x, tile_y, stk_lv, stk_dv, tl);
     add_counters<STATS>(p, threadIdx.x & 63, cnt & CNT_REFL_MASK, cnt >> CNT_SHADOW_SHIFT, tl);
+    if (TORD == 2 && (threadIdx.x & 63) == 0 && t_rec[0].slot != nullptr)
+        *t_rec[0].slot = (unsigned)__builtin_amdgcn_s_memrealtime() - t_rec[0].t0;
 }
-template <int K, bool STATS, bool TILES, int MERGED>
+template <int K, bool STATS, bool TILES, int MERGED, int TORD = 0>
 __global__ __launch_bounds__(WG_THREADS, 8) __attribute__((amdgpu_num_sgpr(80))) void trace_bundle_kernel(
     LaunchParams p) {
-    bundle_kernel_body<K, false, STATS, TILES, MERGED>(p);
+    bundle_kernel_body<K, false, STATS, TILES, MERGED, TORD>(p);
 }
 template <int K, bool STATS, bool TILES, int MERGED>
 __global__ __launch_bounds__(WG_THREADS) void trace_bundle_kernel_gpow(LaunchParams p) {
@@ -1775,6 +1792,14 @@ struct BundleK {
         static constexpr auto fn = GPOW ? trace_bundle_kernel_gpow<K, STATS, TILES, MERGED> : trace_bundle_kernel<K, STATS, TILES, MERGED>;
     };
 };
+// the all-lights-ok merged instantiation's single-frame tile orders (TORD 1 / 2; no GPOW, no diagnostics)
+template <int TORD>
+struct BundleOrdK {
+    template <int K>
+    struct at {
+        static constexpr auto fn = trace_bundle_kernel<K, false, false, 2, TORD>;
+    };
+};
 
 // Scenes with at most DIRECT_SMAX spheres (every BASELINE config of the direct kernel) run a
 // direct kernel whose sphere-pair loops are unrolled.
@@ -1784,8 +1809,13 @@ template <bool GPOW, bool STATS, bool TILES = false>
 static void launch_variant(const LaunchParams& p, bool bundle, dim3 grid, dim3 block, hipStream_t s) {
     if (bundle) {
         // the merged shadow pass's instantiation for S <= 64 spheres and 1..SHADOW_MERGE_L lights
-        if (p.S <= 64 && p.L >= 1 && p.L <= SHADOW_MERGE_L && p.lights_a2_ok)
-            launch_by_depth<BundleK<GPOW, STATS, TILES, 2>::template at>(p, grid, block, s);
+        if (p.S <= 64 && p.L >= 1 && p.L <= SHADOW_MERGE_L && p.lights_a2_ok) {
+            if (!GPOW && !STATS && !TILES && p.tile_cost != nullptr)
+                launch_by_depth<BundleOrdK<2>::template at>(p, grid, block, s);
+            else if (!GPOW && !STATS && !TILES && p.tile_order != nullptr)
+                launch_by_depth<BundleOrdK<1>::template at>(p, grid, block, s);
+            else launch_by_depth<BundleK<GPOW, STATS, TILES, 2>::template at>(p, grid, block, s);
+        }
         else if (p.S <= 64 && p.L >= 1 && p.L <= SHADOW_MERGE_L)
             launch_by_depth<BundleK<GPOW, STATS, TILES, 1>::template at>(p, grid, block, s);
         else
