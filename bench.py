@@ -557,9 +557,18 @@ def main():
     if not args.no_tick and (tick_cfgs or args.config) and world > 1:
         # The plugin path's own multi-GPU Tick() (what RayTracer.Tick with RT_GPUS = N runs): ONE process,
         # Context(N) -- every device traces its interleaved bands and hands them to the host frame over its
-        # own PCIe link.  Rank 0 drives all N devices; the other ranks wait at the barrier.  (The rehearsal
-        # on fewer GPUs: the N workers share the device, RT_CREATE_SHARED_DEVICE.)
-        dist.barrier()
+        # own PCIe link.  Rank 0 drives all N devices; the other ranks wait at a barrier on the host (a gloo
+        # group: an RCCL barrier would leave a spinning collective kernel on each of their GPUs while rank 0's
+        # workers trace there).  (The rehearsal on fewer GPUs: the N workers share the device,
+        # RT_CREATE_SHARED_DEVICE.)
+        torch.cuda.synchronize()
+        host_pg = None
+        if not args.rehearse_gloo:
+            try:  # (every rank calls new_group; a failure falls back to the default group's barrier)
+                host_pg = dist.new_group(backend="gloo")
+            except Exception as e:  # noqa: BLE001
+                print(f"plugin_tick: no gloo group ({e!r}); RCCL barrier instead", file=sys.stderr, flush=True)
+        dist.barrier(group=host_pg)
         if rank == 0:
             try:
                 flags = abi.RT_CREATE_SHARED_DEVICE if args.rehearse_gloo else 0
@@ -572,7 +581,7 @@ def main():
             except Exception as e:  # reported, never fatal for the line
                 pt = {"error": repr(e)}
             out["plugin_tick"] = pt
-        dist.barrier()
+        dist.barrier(group=host_pg)
     if rank == 0:
         print(json.dumps(out), flush=True)
     dist.destroy_process_group()

@@ -270,8 +270,8 @@ def test_single_frame_dispatch_orders(golden, monkeypatch, cid, order):
         ctx.close()
 
 
-@pytest.mark.parametrize("cid", ["C3", "C4"])
-@pytest.mark.parametrize("size", [(203, 117), (8, 8), (9, 300), (1000, 9)])
+@pytest.mark.parametrize("cid,size", [("C3", (203, 117)), ("C3", (8, 8)), ("C3", (9, 300)), ("C3", (1000, 9)),
+                                      ("C4", (203, 117)), ("C4", (8, 8)), ("C4", (9, 300))])
 def test_measured_tile_order_ragged_vs_oracle(oracle, monkeypatch, size, cid):
     """The measured tile order (candidate 3) on frames whose tile count is not a multiple of the 4-tile
     workgroup and whose edge tiles are partial -- the direct kernel (C3's scene) and the bundle kernel (C4's):
