@@ -10,7 +10,7 @@ R=${GRAFT_REPO_ROOT:-/root/repo}
 cd $R
 O=${1:-gpurun_out/check}
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu.log 2>&1 \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread --durations=15 > $O/gpu.log 2>&1 \
     || { echo "GPU TESTS FAILED"; tail -30 $O/gpu.log; exit 1; }
 echo "gpu tests: $(tail -1 $O/gpu.log)"
 timeout -k 10 120 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { cat $O/smoke.log; exit 1; }

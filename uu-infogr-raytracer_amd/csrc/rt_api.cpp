@@ -690,10 +690,19 @@ int tile_order_prepare(rt_ctx* ctx, Device& d, int W, int H, hipStream_t s, Laun
         if (hipStreamSynchronize(s) != hipSuccess ||
             hipMemcpy(cost.data(), o.d_cost, n * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
             return 0;
-        std::vector<uint32_t> idx(n);
-        for (size_t i = 0; i < n; ++i) idx[i] = (uint32_t)i;
-        std::stable_sort(idx.begin(), idx.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
-        for (size_t i = 0; i < n; ++i) order[i] = (uint32_t)((idx[i] / tx) << 16 | (idx[i] % tx));
+        // a stable counting sort by decreasing duration in 16-tick (160 ns) buckets: linear in the tile count
+        // (an 8K frame's 518,400 tiles sort in a few ms instead of tens, once per measuring round)
+        uint32_t cmax = 0;
+        for (size_t i = 0; i < n; ++i) cmax = std::max(cmax, cost[i]);
+        const int shift = cmax >> 4 < (1u << 16) ? 4 : 4 + (32 - __builtin_clz(cmax >> 20 | 1u));
+        const size_t nb = (size_t)(cmax >> shift) + 1;
+        std::vector<uint32_t> start(nb + 1, 0);
+        for (size_t i = 0; i < n; ++i) start[nb - (cost[i] >> shift)]++;  // bucket 0 = the longest
+        for (size_t b = 1; b <= nb; ++b) start[b] += start[b - 1];
+        for (size_t i = 0; i < n; ++i) {
+            const uint32_t t = (uint32_t)i;
+            order[start[nb - 1 - (cost[i] >> shift)]++] = (t / (uint32_t)tx) << 16 | (t % (uint32_t)tx);
+        }
         if (hipMemcpy(o.d_order, order.data(), padded * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) return 0;
         o.built = true;
     }
