@@ -624,13 +624,15 @@ int order_pick(rt_ctx* ctx, Device& d, int W, int H, bool* probe) {
     }
     if (t.chosen >= 0) return t.chosen;
     order_collect(d);
+    // candidate 3 packs tile coordinates in 16 bits each (tile_order_prepare): not for frames beyond that
+    const int nc = (W + 7) / 8 > 0xffff || (H + 7) / 8 > 0xffff ? 3 : ORDER_CANDIDATES;
     bool done = true;
-    for (const std::vector<float>& v : t.ms) done = done && v.size() >= (size_t)ORDER_SAMPLES;
+    for (int k = 0; k < nc; ++k) done = done && t.ms[k].size() >= (size_t)ORDER_SAMPLES;
     if (done) {
         // the least median, unless candidate 0 is within the margin of it: the launches of a bench or of
         // another process on the GPU can overlap the probes, and a noise-driven choice should not stick
         float best = 0, med0 = 0;
-        for (int k = 0; k < ORDER_CANDIDATES; ++k) {
+        for (int k = 0; k < nc; ++k) {
             std::vector<float> v = t.ms[k];
             std::nth_element(v.begin(), v.begin() + v.size() / 2, v.end());
             if (k == 0) med0 = v[v.size() / 2];
@@ -639,7 +641,7 @@ int order_pick(rt_ctx* ctx, Device& d, int W, int H, bool* probe) {
         if (med0 <= best * ORDER_MARGIN) t.chosen = 0;
         return t.chosen;
     }
-    const int k = t.turn++ % ORDER_CANDIDATES;
+    const int k = t.turn++ % nc;
     // bound the probes in flight (results arrive as the launches complete)
     *probe = t.ms[k].size() + t.pending.size() < (size_t)(4 * ORDER_SAMPLES * ORDER_CANDIDATES);
     return k;
