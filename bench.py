@@ -454,6 +454,31 @@ def tick_rates(ctx, W, H, torch, n=20, reps=3, n_single=200):
     return out
 
 
+def lone_frame_rate(ctx, W, H, torch, frames, reps=3, warm=48):
+    """One frame per launch (rt_render_device into HBM, the display loop's shape; never `value`) for an `also`
+    config, counters off: `warm` launches first (the library's dispatch-order tuner measures its candidates and
+    keeps one), then the median of `reps` runs of `frames` launches."""
+    ctx.set_counting(False)
+    dev = torch.empty(W * H, dtype=torch.int32, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+
+    def run(k):
+        for _ in range(k):
+            ctx.render_device(W, H, dev.data_ptr(), st)
+        torch.cuda.synchronize()
+    for _ in range(warm // 8):
+        run(8)
+    rates = []
+    for _ in range(reps):
+        t = time.perf_counter()
+        run(frames)
+        rates.append(frames / (time.perf_counter() - t))
+    ctx.set_counting(True)
+    fps = sorted(rates)[len(rates) // 2]
+    return {"single_launch_fps": fps, "single_launch_ms": 1e3 / fps, "single_launch_fps_runs": [round(r, 1) for r in rates],
+            "dispatch_order": ctx.dispatch_order()}
+
+
 def plugin_ticks(ctx, configs, scenes, n=20, reps=3):
     """The plugin path's Tick() per config (RayTracer.Tick -> rt_render / rt_render_async into registered
     host buffers, the frame complete in host memory -- PCIe included; never `value`), median of `reps` runs
@@ -1257,6 +1282,9 @@ def main_single(args, torch, Context, abi, scenes):
             out["also"][sc2.name] = {k: r2[k] for k in ("value", "unit", "ms_per_step", "fps", "rays_per_frame",
                                                         "workload", "kernel", "kernel_avg_ms", "kernel_ms_per_frame",
                                                         "frames_per_launch", "launches", "hbm_frac")}
+            if not args.no_tick:  # the same config one frame per launch (a display loop's shape, counters off)
+                frames_lone = max(16, min(200, int(0.03 / max(r2["ms_per_step"] / 1e3, 1e-6))))
+                out["also"][sc2.name]["lone_frame"] = lone_frame_rate(ctx, sc2.width, sc2.height, torch, frames_lone)
             # VALU issue (the binding resource) from the committed PMC summary of this config, as for the line
             pmc2 = load_pmc(args.pmc, sc2.name, 1)
             v2 = (pmc2.get("counters") or {}).get("SQ_INSTS_VALU") if pmc2 else None

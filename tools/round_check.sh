@@ -27,7 +27,9 @@ print(sys.argv[2], w, round(d["value"] / 1e3, 1), "Gray/s", round(d["ms_per_step
       round(d.get("tick_async_fps_incl_d2h", 0)), "roofline", round(d["roofline"]["frac"], 4), "valu",
       round(d["roofline_valu"]["frac"] or 0, 3), "order", d.get("dispatch_order"))
 for k, v in d.get("also", {}).items():
-    print("  ", k, round(v["value"] / 1e3, 1), "Gray/s", round(v["ms_per_step"] * 1e3, 2), "us/frame")
+    lone = v.get("lone_frame") or {}
+    print("  ", k, round(v["value"] / 1e3, 1), "Gray/s", round(v["ms_per_step"] * 1e3, 2), "us/frame",
+          f"lone {lone['single_launch_ms'] * 1e3:.1f} us (order {lone['dispatch_order']})" if lone else "")
 for k, v in (d.get("tick_by_config") or {}).items():
     if isinstance(v, dict):
         print("   tick", k, round(v["tick_fps"], 1), "fps sync", round(v["tick_async_fps"], 1), "async",
