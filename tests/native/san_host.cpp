@@ -511,6 +511,41 @@ void check_library() {
 }
 }  // namespace
 
+// tiles_by_cost (the measured dispatch order): a permutation of the tiles, by decreasing cost in the sort's
+// buckets, natural order inside a bucket; costs past 2^20 ticks take wider buckets.
+void check_tiles_by_cost() {
+    uint64_t seed = 12345;
+    auto rnd = [&]() { seed = seed * 6364136223846793005ull + 1442695040888963407ull; return (uint32_t)(seed >> 33); };
+    long checked = 0;
+    for (int trial = 0; trial < 40; ++trial) {
+        const uint32_t tx = 1 + rnd() % 300, ty = 1 + rnd() % 200;
+        const size_t n = (size_t)tx * ty;
+        const uint32_t range = trial % 4 == 0 ? 0xffffffffu : trial % 4 == 1 ? 5000u : trial % 4 == 2 ? (1u << 22) : 17u;
+        std::vector<uint32_t> cost(n), order(n);
+        for (auto& c : cost) c = range == 0xffffffffu ? rnd() * 2u + (rnd() & 1u) : rnd() % (range + 1);
+        tiles_by_cost(cost.data(), n, tx, order.data());
+        uint32_t cmax = 0;
+        for (uint32_t c : cost) cmax = std::max(cmax, c);
+        const int shift = cmax >> 4 < (1u << 16) ? 4 : 4 + (32 - __builtin_clz(cmax >> 20 | 1u));
+        std::vector<char> seen(n, 0);
+        for (size_t k = 0; k < n; ++k) {
+            const uint32_t x = order[k] & 0xffffu, y = order[k] >> 16;
+            CHECK(x < tx && y < ty, "tile in range");
+            const size_t t = (size_t)y * tx + x;
+            CHECK(!seen[t], "each tile once");
+            seen[t] = 1;
+            if (k) {
+                const uint32_t px = order[k - 1] & 0xffffu, py = order[k - 1] >> 16;
+                const size_t pt = (size_t)py * tx + px;
+                const uint32_t b0 = cost[pt] >> shift, b1 = cost[t] >> shift;
+                CHECK(b0 > b1 || (b0 == b1 && pt < t), "decreasing buckets, natural order inside one");
+            }
+        }
+        checked += (long)n;
+    }
+    std::printf("tiles_by_cost: %ld tiles\n", checked);
+}
+
 int main() {
     check_library();
     check_scene_packing();
@@ -518,6 +553,7 @@ int main() {
     check_ppm();
     check_wire_layout();
     check_shadow_threshold();
+    check_tiles_by_cost();
     check_shadow_grid();
     check_ball_cull();
     check_row_order();

@@ -664,6 +664,23 @@ bool order_begin(Device& d, int cand, hipStream_t s) {
 
 void order_end(Device& d, hipStream_t s) { (void)hipEventRecord(d.order.pending.back().b, s); }
 
+// The measured tile order: tiles 0..n-1 (row-major, tx per row) by decreasing cost, ties in natural order, as
+// ty << 16 | tx entries.  A stable counting sort in 16-tick (160 ns) buckets (wider ones past 2^20 ticks): linear
+// in the tile count -- an 8K frame's 518,400 tiles sort in a few ms, once per measuring round.
+void tiles_by_cost(const uint32_t* cost, size_t n, uint32_t tx, uint32_t* order) {
+    uint32_t cmax = 0;
+    for (size_t i = 0; i < n; ++i) cmax = std::max(cmax, cost[i]);
+    const int shift = cmax >> 4 < (1u << 16) ? 4 : 4 + (32 - __builtin_clz(cmax >> 20 | 1u));
+    const size_t nb = (size_t)(cmax >> shift) + 1;
+    std::vector<uint32_t> start(nb + 1, 0);
+    for (size_t i = 0; i < n; ++i) start[nb - (cost[i] >> shift)]++;  // bucket 0 = the longest
+    for (size_t b = 1; b <= nb; ++b) start[b] += start[b - 1];
+    for (size_t i = 0; i < n; ++i) {
+        const uint32_t t = (uint32_t)i;
+        order[start[nb - 1 - (cost[i] >> shift)]++] = (t / tx) << 16 | (t % tx);
+    }
+}
+
 // Candidate 3 of a single-frame launch (the direct kernel's 4-tile workgroups): the first launch of each
 // measuring round (and of each frame size / scene) records every tile's duration instead of being timed as a
 // probe; the first candidate-3 launch after it reads the durations back (one stream synchronisation per
@@ -692,19 +709,7 @@ int tile_order_prepare(rt_ctx* ctx, Device& d, int W, int H, hipStream_t s, Laun
         if (hipStreamSynchronize(s) != hipSuccess ||
             hipMemcpy(cost.data(), o.d_cost, n * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
             return 0;
-        // a stable counting sort by decreasing duration in 16-tick (160 ns) buckets: linear in the tile count
-        // (an 8K frame's 518,400 tiles sort in a few ms instead of tens, once per measuring round)
-        uint32_t cmax = 0;
-        for (size_t i = 0; i < n; ++i) cmax = std::max(cmax, cost[i]);
-        const int shift = cmax >> 4 < (1u << 16) ? 4 : 4 + (32 - __builtin_clz(cmax >> 20 | 1u));
-        const size_t nb = (size_t)(cmax >> shift) + 1;
-        std::vector<uint32_t> start(nb + 1, 0);
-        for (size_t i = 0; i < n; ++i) start[nb - (cost[i] >> shift)]++;  // bucket 0 = the longest
-        for (size_t b = 1; b <= nb; ++b) start[b] += start[b - 1];
-        for (size_t i = 0; i < n; ++i) {
-            const uint32_t t = (uint32_t)i;
-            order[start[nb - 1 - (cost[i] >> shift)]++] = (t / (uint32_t)tx) << 16 | (t % (uint32_t)tx);
-        }
+        tiles_by_cost(cost.data(), n, (uint32_t)tx, order.data());
         if (hipMemcpy(o.d_order, order.data(), padded * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) return 0;
         o.built = true;
     }
