@@ -380,7 +380,9 @@ int rt_set_timing(rt_ctx* ctx, int every);
  * cost, 1 rows bottom to top, 2 rows varying fastest, 3 every tile by decreasing measured duration --
  * the round's first launch records each tile's duration) and keep the fastest; the pixels are the same
  * under every order.  *out_order: the candidate in use, -1 while still measuring (ABI 8 addition;
- * RT_DISPATCH_ORDER=0/1/2/3 in the environment at rt_create fixes it). */
+ * RT_DISPATCH_ORDER=0/1/2/3 in the environment at rt_create fixes it).  The choice is measured again
+ * every 16,384 single-frame launches; candidate 3's tile durations are recorded again once the camera
+ * has moved and 256 launches have used them (one device synchronisation per recording). */
 int rt_dispatch_order(rt_ctx* ctx, int* out_order);
 int rt_get_stats(rt_ctx* ctx, rt_stats* out_stats);
 int rt_reset_stats(rt_ctx* ctx);

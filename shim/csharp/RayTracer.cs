@@ -14,6 +14,7 @@ namespace Template;
 
 internal static class Native {
     private const string Lib = "raytracer_hip";
+    internal const int AbiVersion = 10;  // RT_ABI_VERSION of the include/raytracer_hip.h these declarations follow
 
     [StructLayout(LayoutKind.Sequential)] internal struct Vec3 { public float X, Y, Z; public Vec3(float x, float y, float z) { X = x; Y = y; Z = z; } }
     [StructLayout(LayoutKind.Sequential)] internal struct Material { public Vec3 Kd, Ka, Ks; public float N; public Vec3 Km; }
@@ -22,6 +23,7 @@ internal static class Native {
     [StructLayout(LayoutKind.Sequential)] internal struct Light { public Vec3 Position; public float Intensity; }
     [StructLayout(LayoutKind.Sequential)] internal struct Camera { public Vec3 Position; public float Yaw, Pitch; }
 
+    [DllImport(Lib)] internal static extern int rt_abi_version();
     [DllImport(Lib)] internal static extern int rt_create(int nGpus, out IntPtr ctx);
     [DllImport(Lib)] internal static extern void rt_destroy(IntPtr ctx);
     [DllImport(Lib)] internal static extern IntPtr rt_last_error(IntPtr ctx);
@@ -58,6 +60,11 @@ internal sealed class RayTracer : IDisposable {
 
     public RayTracer(Surface screen) {                    // RayTracer.cs:535-537
         this.screen = screen;
+        // the library must implement the ABI these declarations bind (struct layouts, entry points)
+        int abi = Native.rt_abi_version();
+        if (abi != Native.AbiVersion)
+            throw new InvalidOperationException(
+                $"libraytracer_hip ABI {abi}, this binding needs ABI {Native.AbiVersion}: rebuild or update the library");
         int nGpus = int.TryParse(Environment.GetEnvironmentVariable("RT_GPUS"), out int g) ? g : 1;
         Native.Check(Native.rt_create(nGpus, out _ctx), IntPtr.Zero);
         // the reference's Tick counts no rays: the display loop runs without the library's work counters

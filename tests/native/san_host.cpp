@@ -471,6 +471,77 @@ void check_ball_cull() {
     std::printf("ball_cull: %ld of %ld (sphere, light) pairs culled, every lane checked unblocked\n", culled, pairs);
 }
 
+// The per-lane cluster pre-cull (rt_kernel.hip cluster_mask, restated for one lane in binary32 -- the kernel's
+// rsq by a correctly rounded 1/sqrt, inside the margins): rays from points on and near sphere surfaces and from
+// anywhere in the scene, |d|^2 in [0.5, 2]; for every cluster the lane drops, no member collides under the
+// reference's IntersectsSphere (epsilon 0: neither TracePixel's nor TraceSecondaryRay's rule can select it).
+bool cluster_keeps(const DevCluster& c, rt_vec3 o, rt_vec3 d) {
+    const float a = ((d.x * d.x) + (d.y * d.y)) + (d.z * d.z);
+    const float s = 1.0f / std::sqrt(a);
+    const float A[3] = {d.x * s, d.y * s, d.z * s};
+    const float ol = std::fabs(o.x) + std::fabs(o.y) + std::fabs(o.z);
+    const bool ok = a >= 0.5f && a <= 2.0f && ol < 0x1p40f;
+    const float w[3] = {c.cx - o.x, c.cy - o.y, c.cz - o.z};
+    const float dcl = (std::fabs(w[0]) + std::fabs(w[1]) + std::fabs(w[2])) * (1.0f + 0x1p-20f);
+    const float mgn = 0x1p-8f * (dcl + c.R);
+    const float x[3] = {std::fma(w[1], A[2], -(w[2] * A[1])), std::fma(w[2], A[0], -(w[0] * A[2])),
+                        std::fma(w[0], A[1], -(w[1] * A[0]))};
+    const float T = c.R + mgn;
+    const bool line = std::fma(x[2], x[2], std::fma(x[1], x[1], x[0] * x[0])) > T * T;
+    const bool behind = -std::fma(w[2], A[2], std::fma(w[1], A[1], w[0] * A[0])) - c.R > mgn;
+    const bool valid = dcl >= 0x1p-30f && dcl < 0x1p40f;
+    return !(ok && valid && (line || behind));
+}
+
+void check_cluster_cull() {
+    long culled = 0, tests = 0;
+    for (int it = 0; it < 30; ++it) {
+        const float scale = it % 3 == 2 ? 1000.0f : it % 3 == 1 ? 30.0f : 1.0f;
+        const int S = 12 + (int)(next64() % 53);
+        std::vector<rt_sphere> sph((size_t)S);
+        for (rt_sphere& q : sph) {
+            q.center = v3(unif(-8, 8) * scale, unif(-1, 3) * scale, unif(2, 40) * scale);
+            q.radius = unif(0.05f, 1.5f) * scale;
+            q.material = material((int)(next64() % 5));
+        }
+        rt_light li{v3(-3, 1, -3), 1.0f};
+        rt_ctx ctx;
+        CHECK(rt_set_scene(&ctx, sph.data(), S, nullptr, 0, &li, 1, v3(0.1f, 0.1f, 0.1f), 5) == RT_OK, "scene");
+        const SceneLayout& lay = ctx.layout;
+        CHECK(lay.n_clus == (S + CLUSTER_SIZE - 1) / CLUSTER_SIZE || lay.n_clus > 0, "clusters built for S = %d", S);
+        const DevCluster* cl = (const DevCluster*)(lay.host_blob.data() + lay.off_clus);
+        for (int r = 0; r < 4000; ++r) {
+            rt_vec3 o;
+            if (r % 2 == 0) {  // on / near a sphere surface (a reflected segment's origin)
+                const rt_sphere& s0 = sph[next64() % (size_t)S];
+                const double d0[3] = {unif(-1, 1), unif(-1, 1), unif(-1, 1)};
+                const double n0 = std::sqrt(d0[0] * d0[0] + d0[1] * d0[1] + d0[2] * d0[2]) + 1e-30;
+                const double rr0 = (double)s0.radius * (1.0 + unif(-1e-6f, 1e-3f));
+                o = v3((float)(s0.center.x + rr0 * d0[0] / n0), (float)(s0.center.y + rr0 * d0[1] / n0),
+                       (float)(s0.center.z + rr0 * d0[2] / n0));
+            } else {
+                o = v3(unif(-10, 10) * scale, unif(-2, 5) * scale, unif(-5, 45) * scale);
+            }
+            double dd[3] = {unif(-1, 1), unif(-1, 1), unif(-1, 1)};
+            const double dn = std::sqrt(dd[0] * dd[0] + dd[1] * dd[1] + dd[2] * dd[2]) + 1e-30;
+            const double len = std::sqrt((double)unif(0.5f, 2.0f));
+            const rt_vec3 d = v3((float)(dd[0] / dn * len), (float)(dd[1] / dn * len), (float)(dd[2] / dn * len));
+            for (int j = 0; j < lay.n_clus; ++j) {
+                ++tests;
+                if (cluster_keeps(cl[j], o, d)) continue;
+                ++culled;
+                for (int i = 0; i < S; ++i) {
+                    if (!((cl[j].members >> i) & 1ull)) continue;
+                    int col = 0;
+                    oracle_intersect_sphere(o, d, sph[(size_t)i].center, sph[(size_t)i].radius, 0.0f, &col);
+                    CHECK(!col, "scene %d ray %d: cluster %d culled but sphere %d collides", it, r, j, i);
+                }
+            }
+        }
+    }
+    std::printf("cluster_cull: %ld of %ld (ray, cluster) tests culled, every member checked\n", culled, tests);
+}
+
 // Single-frame row order (row_order): a floor below the camera fills the bottom rows (high y), so they
 // are dispatched first; a ceiling above it puts the top rows first; with no plane and no sphere every
 // row costs the same and the order stays natural.
@@ -546,8 +617,58 @@ void check_tiles_by_cost() {
     std::printf("tiles_by_cost: %ld tiles\n", checked);
 }
 
+// build_clusters (the bundle kernel's per-lane pre-cull): the clusters partition the spheres, hold at most
+// `size` members each, and every member's ball (centre, cull radius r') lies inside its cluster's bounding
+// sphere, checked in double from the float records the kernel reads; a member with an unusable record
+// (NaN / infinite centre or radius) leaves its cluster's R NaN (never culled).
+void check_clusters() {
+    long checked = 0;
+    for (int trial = 0; trial < 300; ++trial) {
+        const int S = 1 + (int)(next64() % 64), size = 1 + (int)(next64() % 8);
+        const float scale = trial % 3 == 0 ? 1.0f : trial % 3 == 1 ? 30.0f : 1000.0f;
+        std::vector<DevSphereCull> cull((size_t)S);
+        for (int i = 0; i < S; ++i) {
+            const float r = unif(0.001f, 1.0f) * scale;
+            cull[(size_t)i] = DevSphereCull{unif(-8, 8) * scale, unif(-1, 1) * scale, unif(4, 32) * scale,
+                                            std::nextafter((float)(std::sqrt((double)(r * r)) * (1.0 + 0x1p-8)), INFINITY)};
+            if (trial % 7 == 3 && i == S / 2) cull[(size_t)i].cx = trial % 2 ? NAN : INFINITY;  // unusable record
+            if (trial % 11 == 5 && i == 0) cull[(size_t)i].rr = NAN;
+        }
+        DevCluster c[MAX_CLUSTERS];
+        const int n = build_clusters(cull.data(), S, size, c);
+        if ((S + size - 1) / size > MAX_CLUSTERS) {  // (median splits give at most 2 S / size groups)
+            CHECK(n == 0 || n <= MAX_CLUSTERS, "cluster count within the table");
+            if (n == 0) continue;
+        }
+        CHECK(n >= 1 && n <= MAX_CLUSTERS, "cluster count %d (S %d size %d)", n, S, size);
+        unsigned long long all = 0;
+        for (int j = 0; j < n; ++j) {
+            CHECK((all & c[j].members) == 0, "clusters disjoint");
+            all |= c[j].members;
+            CHECK(__builtin_popcountll(c[j].members) <= size && c[j].members != 0, "cluster size");
+            bool usable = true;
+            for (int i = 0; i < S; ++i) {
+                if (!((c[j].members >> i) & 1ull)) continue;
+                const DevSphereCull& s = cull[(size_t)i];
+                if (!(std::isfinite(s.cx) && std::isfinite(s.cy) && std::isfinite(s.cz) && std::isfinite(s.rr))) {
+                    usable = false;
+                    continue;
+                }
+                const double dx = (double)s.cx - c[j].cx, dy = (double)s.cy - c[j].cy, dz = (double)s.cz - c[j].cz;
+                CHECK(std::sqrt(dx * dx + dy * dy + dz * dz) + (double)s.rr <= (double)c[j].R || std::isnan(c[j].R),
+                      "member ball inside the cluster bound");
+                ++checked;
+            }
+            CHECK(usable || std::isnan(c[j].R), "unusable member -> NaN bound");
+        }
+        CHECK(all == (S == 64 ? ~0ull : (1ull << S) - 1ull), "every sphere in one cluster");
+    }
+    std::printf("clusters: %ld member bounds\n", checked);
+}
+
 int main() {
     check_library();
+    check_clusters();
     check_scene_packing();
     check_camera_input();
     check_ppm();
@@ -556,6 +677,7 @@ int main() {
     check_tiles_by_cost();
     check_shadow_grid();
     check_ball_cull();
+    check_cluster_cull();
     check_row_order();
     std::printf("san_host: %d failures\n", failures);
     return failures ? 1 : 0;

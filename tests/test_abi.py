@@ -28,6 +28,19 @@ def test_header_declares_expected_api():
     assert set(names) == {n for n, _, _ in abi.EXPORTS}
 
 
+def test_csharp_shim_binds_declared_entry_points_and_checks_the_abi():
+    """shim/csharp/RayTracer.cs: every [DllImport] is an entry point the header declares, and the constructor
+    compares rt_abi_version() with the ABI the binding was written for (RT_ABI_VERSION) before anything else."""
+    src = open(os.path.join(ROOT, "shim", "csharp", "RayTracer.cs")).read()
+    externs = re.findall(r"\[DllImport\(Lib\)\]\s+internal static extern \w+ (rt_\w+)\(", src)
+    assert externs and set(externs) <= set(declared_functions()), set(externs) - set(declared_functions())
+    assert "rt_abi_version" in externs
+    want = int(re.search(r"#define RT_ABI_VERSION (\d+)", open(HEADER).read()).group(1))
+    assert int(re.search(r"internal const int AbiVersion = (\d+);", src).group(1)) == want == abi.RT_ABI_VERSION
+    ctor = src[src.index("public RayTracer(Surface screen)"):]
+    assert ctor.index("rt_abi_version()") < ctor.index("rt_create(")
+
+
 def test_library_exports_every_declared_symbol(rtlib):
     out = subprocess.run(["nm", "-D", "--defined-only", abi.LIB_PATH], capture_output=True, text=True,
                          check=True).stdout

@@ -146,6 +146,21 @@ def test_shadow_grid_scenes_vs_oracle(gpu_ctx, oracle, seed, monkeypatch):
         assert ray_counts(st) == ray_counts(ost)
 
 
+@pytest.mark.parametrize("seed", list(range(24)))
+def test_trace_cluster_precull_vs_oracle(gpu_ctx, oracle, seed, monkeypatch):
+    """The bundle kernel's per-lane cluster pre-cull of trace bundles too wide for the bundle cull (rt_kernel.hip
+    cluster_mask; clusters of RT_TRACE_CLUSTERS spheres built at rt_set_scene, 0 = off): the mirror-heavy grid
+    scenes at unit, 30x and 1000x scale, clusters of 2, 4 (the default) and 8 spheres and none -- every pixel
+    and ray count the oracle's."""
+    sc = shadow_grid_scene(1000 + seed, 128, 80)
+    want, ost = oracle.render(sc, oracle.MODE_NEAREST, 8)
+    for z in ("4", "2", "8", "0"):
+        monkeypatch.setenv("RT_TRACE_CLUSTERS", z)
+        px, st = render_gpu(gpu_ctx, sc)
+        assert_same(px, want, f"{sc.name} RT_TRACE_CLUSTERS={z}")
+        assert ray_counts(st) == ray_counts(ost)
+
+
 @pytest.mark.parametrize("n_lights", [3000, 4200])
 def test_many_lights_with_and_without_the_shadow_cull_table(gpu_ctx, oracle, n_lights):
     """The bundle kernel's shadow culling reads the sphere centres pre-projected into each light's
@@ -351,6 +366,89 @@ def test_dispatch_order_measured_then_kept(golden):
             assert ctx.dispatch_order() in (0, 1, 2, 3)
             for o in outs:
                 assert crc(o.cpu().numpy()) == e["crc32"]
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("cid", ["C3", "C4"])
+def test_measured_tile_order_mixed_streams_and_sizes(oracle, monkeypatch, cid):
+    """The measured order (candidate 3) with single-frame launches on two streams and alternating frame sizes,
+    no rt_wait between them: rt_render_async frames on the library's async stream and rt_render_device frames on
+    a torch stream, each size change recording the tile durations again and rebuilding the order while the other
+    stream's launches may still read it (tile_order_prepare waits for the whole device first).  Every frame =
+    the oracle's."""
+    import torch
+    monkeypatch.setenv("RT_DISPATCH_ORDER", "3")
+    sizes = [(203, 117), (160, 96)]
+    scs = [scenes.config(cid).resized(*s) for s in sizes]
+    wants = [oracle.render(s, oracle.MODE_NEAREST, 8)[0] for s in scs]
+    ctx = Context(1)
+    hosts = [np.zeros(w * h, dtype=np.int32) for (w, h) in sizes for _ in range(3)]
+    try:
+        ctx.set_scene(scs[0])  # (the two sizes share the scene; rt_set_scene of either is the same tables)
+        for hb in hosts:
+            ctx.register_host(hb)
+        W1, H1 = sizes[1]
+        outs = [torch.zeros(W1 * H1, dtype=torch.int32, device="cuda") for _ in range(3)]
+        s = torch.cuda.Stream()
+        for k in range(3):
+            ctx.render_async(*sizes[0], hosts[k])  # size 0, async stream
+            ctx.render_device(W1, H1, outs[k].data_ptr(), s.cuda_stream)  # size 1, another stream
+        ctx.wait()
+        s.synchronize()
+        for k in range(3):
+            assert_same(hosts[k].reshape(sizes[0][1], sizes[0][0]), wants[0], f"{cid} async frame {k}")
+            assert_same(outs[k].cpu().numpy().reshape(H1, W1), wants[1], f"{cid} device frame {k}")
+        assert ctx.dispatch_order() == 3
+    finally:
+        for hb in hosts:
+            ctx.unregister_host(hb)
+        ctx.close()
+
+
+@pytest.mark.parametrize("order", ["0", "3", None])
+@pytest.mark.parametrize("cid", ["C2", "C3", "C4"])
+def test_view_height_cut_frames_are_the_full_frames_rows(oracle, monkeypatch, cid, order):
+    """rt_set_view_height (ABI 9): a W x H' render under a W x VH view (H' < VH) is rows [0, H') of the W x VH
+    frame -- one-frame launches (rt_render, rt_render_device) under the dispatch orders 0 and 3 and the library's
+    own choice, and band renders (8-row bands of 3 ranks into a row-major frame); H' > VH is an invalid argument.
+    The direct kernel (C2, C3) and the bundle kernel (C4)."""
+    import torch
+    if order is None:
+        monkeypatch.delenv("RT_DISPATCH_ORDER", raising=False)
+    else:
+        monkeypatch.setenv("RT_DISPATCH_ORDER", order)
+    W, VH = 240, 136
+    sc = scenes.config(cid).resized(W, VH)
+    want, _ = oracle.render(sc, oracle.MODE_NEAREST, 8)
+    ctx = Context(1)
+    try:
+        ctx.set_scene(sc)
+        ctx.set_view_height(VH)
+        st = torch.cuda.current_stream().cuda_stream
+        for Hc in (VH, 99, 64, 1):
+            for _ in range(2 if order is not None else 1):
+                assert_same(ctx.render(W, Hc).copy(), want[:Hc], f"{cid} rt_render {W}x{Hc} of {W}x{VH}")
+            out = torch.zeros(W * Hc, dtype=torch.int32, device="cuda")
+            for _ in range(60 if order is None else 2):  # (None: past the tuner's probes and its recording)
+                ctx.render_device(W, Hc, out.data_ptr(), st)
+            torch.cuda.synchronize()
+            assert_same(out.cpu().numpy().reshape(Hc, W), want[:Hc], f"{cid} rt_render_device {W}x{Hc}")
+            # the tuner's choice reads as made (the bundle kernel's cut frames are single-frame launches too; the
+            # direct kernel's only at the full view height)
+            if order is None and Hc > 8 and (cid == "C4" or Hc == VH):
+                assert ctx.dispatch_order() in (0, 1, 2, 3), "a chosen order reads as still measuring"
+            frame = torch.zeros(W * Hc, dtype=torch.int32, device="cuda")
+            for r in range(3):
+                ctx.render_bands_ex(W, Hc, 8, r, 3, frame.data_ptr(), abi.RT_BANDS_FRAME, st)
+            torch.cuda.synchronize()
+            assert_same(frame.cpu().numpy().reshape(Hc, W), want[:Hc], f"{cid} bands {W}x{Hc}")
+        with pytest.raises(abi.RayTracerError) as ei:
+            ctx.render(W, VH + 1)
+        assert ei.value.code == abi.RT_ERR_INVALID_ARG
+        ctx.set_view_height(0)  # back to the frame's own view
+        small = scenes.config(cid).resized(W, 64)
+        assert_same(ctx.render(W, 64).copy(), oracle.render(small, oracle.MODE_NEAREST, 8)[0], f"{cid} view reset")
     finally:
         ctx.close()
 

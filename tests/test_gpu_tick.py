@@ -147,9 +147,9 @@ def test_tick_chunked_golden(golden, chunks_env, copy_env, cid, world, chunks, m
 
 @pytest.mark.parametrize("world", [1, 3, 8])
 def test_tick_unregistered_buffer(golden, world):
-    """An unregistered host buffer: each worker's bands by the runtime's copies, one per band (nothing
-    written outside the frame: a pitched 2-D copy into pageable memory left the process aborting at exit
-    with a corrupted heap in r05b)."""
+    """An unregistered host buffer: each worker's bands by the runtime's copies, one per band, and nothing
+    written outside the frame (a pitched 2-D copy into pageable memory is not used: nothing bounds what its
+    staging writes past the last row; it was not the cause of r05b's exit abort, profiles/r06_exit_abort.txt)."""
     e = golden["cases"]["C3"]
     sc = scenes.config("C3")
     with Context(world, abi.RT_CREATE_SHARED_DEVICE) as ctx:
@@ -280,3 +280,32 @@ def test_shared_device_refuses_rccl_gather():
     with pytest.raises(RayTracerError) as ei:
         Context(2, abi.RT_CREATE_SHARED_DEVICE | abi.RT_CREATE_RCCL_GATHER)
     assert ei.value.code == abi.RT_ERR_INVALID_ARG
+
+
+CHILD_RCCL_THEN_TORCH = r"""
+import os, sys
+sys.path.insert(0, os.path.join(sys.argv[1], "uu-infogr-raytracer_amd"))
+from raytracer_hip import Context, abi, scenes
+sc = scenes.config("C2").resized(320, 180)
+with Context(1, abi.RT_CREATE_RCCL_GATHER) as c:  # loads librccl (our dlopen) before torch does
+    c.set_scene(sc)
+    c.render(sc.width, sc.height)
+import torch  # torch's own librccl
+torch.zeros(1, device="cuda").add_(1).sum().item()
+print("child done", flush=True)
+"""
+
+
+def test_rccl_then_torch_in_a_fresh_process_exits_cleanly():
+    """Round 5's exit abort in the order that produced it (profiles/r06_exit_abort.txt): a fresh interpreter loads
+    RCCL through an RCCL-gather context and renders, then imports torch and runs one GPU op, then exits -- status
+    0 and no glibc heap message.  (The parent pytest process may have imported torch already, which hides the
+    order; the child starts clean and the parent makes no GPU call for it.)"""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", CHILD_RCCL_THEN_TORCH, root], capture_output=True, text=True, timeout=110)
+    err = r.stderr.lower()
+    assert r.returncode == 0, f"rc {r.returncode}: {r.stderr[-2000:]}"
+    assert "child done" in r.stdout
+    assert "double free" not in err and "corruption" not in err, r.stderr[-2000:]

@@ -1,5 +1,7 @@
-"""r05: which sequence leaves the process aborting at exit (glibc "double free or corruption" after the Tick
-tests, r05b).  One sequence per process:  python tools/probes/exit_abort_probe.py A|B|C|D|E|F|G"""
+"""r05/r06: which sequence leaves the process aborting at exit (glibc "double free or corruption" after the Tick
+tests, r05b).  One sequence per process:  python tools/probes/exit_abort_probe.py A|B|...|I
+RAYTRACER_HIP_LIB selects the library build (tools/probes/exit_abort.sh runs the product build and the two
+pre-fix variants, tools/probes/rtld_global.patch and pitched_pageable.patch, over every sequence)."""
 import os
 import sys
 
@@ -32,7 +34,11 @@ def plain(n=1, flags=0, register=True):
 
 seq = {"A": [rccl, plain], "B": [rccl, lambda: plain(2, abi.RT_CREATE_SHARED_DEVICE)],
        "C": [rccl, lambda: plain(1, 0, False)], "D": [lambda: plain(2, abi.RT_CREATE_SHARED_DEVICE), rccl],
-       "E": [rccl, rccl], "F": [rccl], "G": [rccl, lambda: __import__("torch").zeros(1, device="cuda").sum().item()]
+       "E": [rccl, rccl], "F": [rccl], "G": [rccl, lambda: __import__("torch").zeros(1, device="cuda").sum().item()],
+       # H: an unregistered frame of a 3-worker shared-device Tick (one runtime copy per band; the pitched 2-D
+       # copy into pageable memory in the pitched_pageable build); I: torch imported after RCCL, no GPU op
+       "H": [lambda: plain(3, abi.RT_CREATE_SHARED_DEVICE, False)],
+       "I": [rccl, lambda: __import__("torch")],
        }[sys.argv[1]]
 for f in seq:
     f()

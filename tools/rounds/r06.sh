@@ -1,0 +1,48 @@
+#!/bin/bash
+# Round-6 GPU runs (through gpurun), one step per call:  bash tools/rounds/r06.sh STEP
+# Every GPU step has its own time limit; a failed step ends the call.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-/root/repo}
+cd $R
+O=gpurun_out/r06
+mkdir -p $O
+case $1 in
+a)  # exit-abort cause (product vs the two pre-fix builds), deep-Tick first-run probe, 1080p Tick chunk sweep
+    bash tools/probes/exit_abort.sh $O/exit_abort > $O/exit_abort.txt 2>&1; rc=$?; cat $O/exit_abort.txt; [ $rc -eq 0 ] || exit 1
+    timeout -k 10 300 python -u tools/tick_deep_probe.py deep > $O/tick_deep.txt 2>&1 || { tail $O/tick_deep.txt; exit 1; }
+    cat $O/tick_deep.txt
+    timeout -k 10 300 python -u tools/tick_deep_probe.py chunks > $O/tick_chunks.txt 2>&1 || { tail $O/tick_chunks.txt; exit 1; }
+    cat $O/tick_chunks.txt
+    ;;
+b)  # the GPU suite on the cluster pre-cull build, then wall per frame with the pre-cull off / cluster sizes 2, 4
+    # (default), 8 -- one library, RT_TRACE_CLUSTERS read at rt_set_scene; 64-frame launches, two interleaved passes
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_b.log 2>&1 \
+        || { echo "GPU TESTS FAILED"; tail -30 $O/gpu_b.log; exit 1; }
+    echo "gpu tests: $(tail -1 $O/gpu_b.log)"
+    for c in C4 C5; do for rep in 1 2; do for z in 0 2 4 8; do
+        echo -n "$c z=$z "
+        RT_TRACE_CLUSTERS=$z timeout -k 10 180 python tools/frame_wall.py --config $c --batch 64 --frames 1024 2>&1 | grep -v amdgpu.ids | tail -1 || exit 1
+    done; done; done | tee $O/clusters_wall.txt
+    ;;
+c)  # the device's f64 pow against glibc (tools/pow_check.hip, built on the CPU side); cluster sizes by wall and PMC
+    # (one-frame C4 launches: VALU / SALU / SMEM, issue stalls); the deep Tick of the bench under a HIP API trace
+    timeout -k 10 600 ./tools/pow_check > $O/pow_check.txt 2>&1; rc=$?; tail -12 $O/pow_check.txt; [ $rc -le 1 ] || exit 1
+    for c in C4 C5; do for rep in 1 2; do for z in 0 4 8 12 16; do
+        echo -n "$c z=$z "
+        RT_TRACE_CLUSTERS=$z timeout -k 10 180 python tools/frame_wall.py --config $c --batch 64 --frames 1024 2>&1 | grep -v amdgpu.ids | tail -1 || exit 1
+    done; done; done | tee $O/clusters_wall_c.txt
+    export TMPDIR=/tmp
+    for z in 0 8; do
+        rm -rf $O/pmc_z$z
+        RT_TRACE_CLUSTERS=$z timeout -s KILL 90 rocprofv3 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_WAIT_INST_ANY SQ_WAVES \
+            --output-format csv -d $O/pmc_z$z -o run -- python3 tools/frame_wall.py --config C4 --frames 20 --reps 1 > $O/pmc_z$z.log 2>&1 \
+            || { tail -5 $O/pmc_z$z.log; exit 1; }
+        echo "== C4 RT_TRACE_CLUSTERS=$z"; python3 tools/pmc_summary.py $O/pmc_z$z | grep -v "HBM\|utilisation"
+    done | tee $O/clusters_pmc.txt
+    rm -rf $O/tick_trace
+    timeout -k 10 300 rocprofv3 --hip-runtime-trace --kernel-trace --memory-copy-trace --output-format csv -d $R/$O/tick_trace -o tick \
+        -- python3 $R/tools/tick_deep_probe.py deep --variants bench --runs 4 > $O/tick_trace.log 2>&1 || { tail $O/tick_trace.log; exit 1; }
+    cat $O/tick_trace.log
+    ;;
+*)  echo "unknown step $1"; exit 2 ;;
+esac

@@ -77,8 +77,9 @@ struct Rccl {
         dl_iterate_phdr(find_loaded_rccl, &loaded);
         if (!loaded.empty()) h = dlopen(loaded.c_str(), RTLD_NOW | RTLD_NOLOAD);
         // RTLD_LOCAL: a RCCL loaded here must not interpose on one the process loads later (torch's own
-        // librccl, pulled in by an `import torch` after our first multi-GPU context): with RTLD_GLOBAL the
-        // two copies shared symbols and the process aborted at exit ("double free or corruption", r05b)
+        // librccl, pulled in by an `import torch` after our first RCCL context): with RTLD_GLOBAL the two
+        // copies shared symbols and the process aborted at exit ("double free or corruption (!prev)", r05b) --
+        // the one cause, profiles/r06_exit_abort.txt (RCCL then `import torch` aborts under RTLD_GLOBAL only)
         const char* names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1"};
         for (const char* n : names)
             if (!h && (h = dlopen(n, RTLD_NOW | RTLD_LOCAL))) break;
@@ -175,6 +176,8 @@ struct Device {
             int W = 0, H = 0;
             uint64_t gen = 0, scene_gen = 0;
             bool recorded = false, built = false;
+            rt_camera cam{};         // the camera of the recorded durations
+            uint64_t uses = 0;       // candidate-3 launches since they were recorded
             uint32_t* d_order = nullptr;  // padded to SINGLE_WPG (ty = 0xffff past the last tile)
             uint32_t* d_cost = nullptr;   // RTC ticks per tile
             size_t order_cap = 0, cost_cap = 0;
@@ -193,7 +196,8 @@ struct Device {
 struct SceneLayout {
     int S = 0, P = 0, L = 0, limit = 0;
     size_t off_sph = 0, off_mat = 0, off_pl = 0, off_li = 0, off_cull = 0, off_shcull = 0, bytes = 0;
-    size_t off_shg = 0, off_shgrid = 0, off_shslab = 0;
+    size_t off_shg = 0, off_shgrid = 0, off_shslab = 0, off_clus = 0;
+    int n_clus = 0;  // DevCluster records (the bundle kernel's per-lane pre-cull), 0: none
     bool has_shcull = false;
     bool has_shg = false;  // per-light shadow grids (DevShadowGrid) for the merged shadow pass
     std::vector<unsigned char> host_blob;  // the uploaded scene image (host tests read the tables)
@@ -544,6 +548,8 @@ void scene_params(const rt_ctx* ctx, const Device& d, LaunchParams& lp) {
     lp.shg = L.has_shg ? (const DevShadowGrid*)(base + L.off_shg) : nullptr;
     lp.shgrid = L.has_shg ? (const unsigned long long*)(base + L.off_shgrid) : nullptr;
     lp.shslab = L.has_shg ? (const unsigned long long*)(base + L.off_shslab) : nullptr;
+    lp.clus = L.n_clus ? (const DevCluster*)(base + L.off_clus) : nullptr;
+    lp.n_clus = L.n_clus;
     lp.S = L.S, lp.P = L.P, lp.L = L.L, lp.limit = L.limit;
     lp.lights_a2_ok = L.lights_a2_ok ? 1 : 0;
     lp.counters = ctx->counting ? d.d_counters : nullptr;  // nullptr: the kernels count nothing (rt_set_counting)
@@ -683,12 +689,18 @@ void tiles_by_cost(const uint32_t* cost, size_t n, uint32_t tx, uint32_t* order)
 
 // Candidate 3 of a single-frame launch (the direct kernel's 4-tile workgroups): the first launch of each
 // measuring round (and of each frame size / scene) records every tile's duration instead of being timed as a
-// probe; the first candidate-3 launch after it reads the durations back (one stream synchronisation per
-// round) and uploads the tiles sorted by decreasing duration, ties in natural order.  Returns the candidate
-// to launch (candidate 3 falls back to 0 while its order is not ready).
-int tile_order_prepare(rt_ctx* ctx, Device& d, int W, int H, hipStream_t s, LaunchParams& lp, int cand, bool* probe) {
+// probe; the first candidate-3 launch after it reads the durations back and uploads the tiles sorted by
+// decreasing duration, ties in natural order.  The readback and the upload wait for the whole device (once
+// per measuring round): the recording launch and the launches still reading the previous order may sit on
+// any stream of the context (d.stream, the async stream, a caller's stream of rt_render_device).  The order
+// is recorded again when the camera has moved and TILE_ORDER_REFRESH launches have used it (an interactive
+// view drifts; pixels never depend on the order).  Returns the candidate to launch (candidate 3 falls back to
+// 0 while its order is not ready), -1 when the buffers cannot be allocated, -2 on a HIP error (recorded).
+constexpr uint64_t TILE_ORDER_REFRESH = 256;
+int tile_order_prepare(rt_ctx* ctx, Device& d, int W, int H, LaunchParams& lp, int cand, bool* probe) {
     Device::OrderTuner::Tiles& o = d.order.tiles;
-    if (o.gen != d.order.gen || o.scene_gen != ctx->scene_gen || o.W != W || o.H != H) {
+    if (o.gen != d.order.gen || o.scene_gen != ctx->scene_gen || o.W != W || o.H != H ||
+        (o.built && o.uses >= TILE_ORDER_REFRESH && std::memcmp(&o.cam, &ctx->cam, sizeof o.cam) != 0)) {
         o.gen = d.order.gen, o.scene_gen = ctx->scene_gen, o.W = W, o.H = H;
         o.recorded = o.built = false;
     }
@@ -701,19 +713,28 @@ int tile_order_prepare(rt_ctx* ctx, Device& d, int W, int H, hipStream_t s, Laun
         if (rc != RT_OK) return -1;
         lp.tile_cost = o.d_cost;
         o.recorded = true;
+        o.cam = ctx->cam, o.uses = 0;
         *probe = false;  // (the duration stores are not the candidate's own cost)
         return cand == 3 ? 0 : cand;
     }
     if (cand == 3 && !o.built) {
         std::vector<uint32_t> cost(n), order(padded, 0xffff0000u);
-        if (hipStreamSynchronize(s) != hipSuccess ||
-            hipMemcpy(cost.data(), o.d_cost, n * sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
-            return 0;
-        tiles_by_cost(cost.data(), n, (uint32_t)tx, order.data());
-        if (hipMemcpy(o.d_order, order.data(), padded * sizeof(uint32_t), hipMemcpyHostToDevice) != hipSuccess) return 0;
+        hipError_t e = hipDeviceSynchronize();
+        if (e == hipSuccess) e = hipMemcpy(cost.data(), o.d_cost, n * sizeof(uint32_t), hipMemcpyDeviceToHost);
+        if (e == hipSuccess) {
+            tiles_by_cost(cost.data(), n, (uint32_t)tx, order.data());
+            e = hipMemcpy(o.d_order, order.data(), padded * sizeof(uint32_t), hipMemcpyHostToDevice);
+        }
+        if (e != hipSuccess) {
+            fail(ctx, RT_ERR_HIP, "tile order readback / upload: %s", hipGetErrorString(e));
+            return -2;
+        }
         o.built = true;
     }
-    if (cand == 3) lp.tile_order = o.d_order;
+    if (cand == 3) {
+        lp.tile_order = o.d_order;
+        o.uses++;
+    }
     return cand;
 }
 
@@ -758,7 +779,8 @@ int trace_bands(rt_ctx* ctx, Device& d, hipStream_t stream, int W, int H, int ba
         cand = order_pick(ctx, d, W, H, &probe);
         // (candidates 1 and 2 order the direct kernel's 4-tile groups: a bundle launch under them is natural order)
         if (ctx->order_fixed < 0 ? d.order.chosen < 0 || cand == 3 : cand == 3)  // measuring, or the measured order
-            cand = tile_order_prepare(ctx, d, W, H, stream, lp, cand, &probe);
+            cand = tile_order_prepare(ctx, d, W, H, lp, cand, &probe);
+        if (cand == -2) return RT_ERR_HIP;  // (rt_last_error holds the HIP error)
         if (cand < 0) return fail(ctx, RT_ERR_OOM, "tile order buffers");
         if (lone && cand == 1)
             for (int r = 0; r < lp.row_order_n; ++r) lp.row_order[r] = (uint16_t)(lp.row_order_n - 1 - r);
@@ -1131,6 +1153,66 @@ float up(double v) { float f = (float)v; return (double)f < v ? std::nextafter(f
 // a_f - (far_k |hp|_1 - 2^-8 B), which raises the slab rule's margin from B to |hp|_1.  Spheres
 // without a valid record (NaN/inf, r^2 < 2^-100, |C|_1 >= 2^30) are never culled (`always`); a
 // light whose |p|^2 lies outside [2^-40, 2^40] (the analysis' range) culls nothing.
+// The bundle kernel's sphere clusters (rt_internal.h DevCluster): median splits of the sphere centres along the
+// widest axis of their box until a group holds at most `size` spheres; each cluster's centre is the middle of
+// its members' box (rounded to float) and R, computed in double from that rounded centre and rounded up, bounds
+// |c_i - centre| + r'_i for every member (r' = the DevSphereCull radius, itself >= r (1 + 2^-8)).  A member
+// without a usable cull record (NaN / infinite centre or radius) makes its cluster's R NaN: never culled.
+// Returns the cluster count (<= MAX_CLUSTERS).
+int build_clusters(const DevSphereCull* cull, int S, int size, DevCluster* out) {
+    std::vector<std::vector<int>> todo(1, std::vector<int>((size_t)S)), groups;
+    for (int i = 0; i < S; ++i) todo[0][(size_t)i] = i;
+    while (!todo.empty()) {
+        std::vector<int> g = std::move(todo.back());
+        todo.pop_back();
+        if ((int)g.size() <= size) {
+            groups.push_back(std::move(g));
+            continue;
+        }
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        for (int i : g) {
+            const double c[3] = {cull[i].cx, cull[i].cy, cull[i].cz};
+            for (int k = 0; k < 3; ++k) lo[k] = std::fmin(lo[k], c[k]), hi[k] = std::fmax(hi[k], c[k]);
+        }
+        int ax = 0;
+        for (int k = 1; k < 3; ++k)
+            if (hi[k] - lo[k] > hi[ax] - lo[ax]) ax = k;
+        auto key = [&](int i) {  // (NaN last: a strict weak order for the sort)
+            const float k = ax == 0 ? cull[i].cx : ax == 1 ? cull[i].cy : cull[i].cz;
+            return std::isnan(k) ? INFINITY : k;
+        };
+        std::stable_sort(g.begin(), g.end(), [&](int a, int b) { return key(a) < key(b); });
+        const size_t h = g.size() / 2;
+        todo.emplace_back(g.begin(), g.begin() + (long)h);
+        todo.emplace_back(g.begin() + (long)h, g.end());
+    }
+    if ((int)groups.size() > MAX_CLUSTERS) return 0;
+    int n = 0;
+    for (const std::vector<int>& g : groups) {
+        double lo[3] = {INFINITY, INFINITY, INFINITY}, hi[3] = {-INFINITY, -INFINITY, -INFINITY};
+        bool usable = true;
+        unsigned long long m = 0;
+        for (int i : g) {
+            const double c[3] = {cull[i].cx, cull[i].cy, cull[i].cz};
+            for (int k = 0; k < 3; ++k) lo[k] = std::fmin(lo[k], c[k]), hi[k] = std::fmax(hi[k], c[k]);
+            usable = usable && std::isfinite(c[0]) && std::isfinite(c[1]) && std::isfinite(c[2]) &&
+                     std::isfinite((double)cull[i].rr) && cull[i].rr >= 0x1p-50f;
+            m |= 1ull << i;
+        }
+        DevCluster& c = out[n++];
+        c.cx = (float)((lo[0] + hi[0]) / 2), c.cy = (float)((lo[1] + hi[1]) / 2), c.cz = (float)((lo[2] + hi[2]) / 2);
+        double R = 0;
+        for (int i : g) {
+            const double dx = (double)cull[i].cx - c.cx, dy = (double)cull[i].cy - c.cy, dz = (double)cull[i].cz - c.cz;
+            R = std::fmax(R, std::sqrt(dx * dx + dy * dy + dz * dz) + (double)cull[i].rr);
+        }
+        c.R = usable && R < 0x1p40 ? std::nextafter((float)(R * (1.0 + 0x1p-20)), INFINITY) : NAN;
+        c.members = m;
+        c.pad = 0;
+    }
+    return n;
+}
+
 void build_shadow_grid(const DevLight& l, const Frame3& f, const DevSphere* sph, const DevSphereCull* cull, int S,
                        DevShadowGrid& g, unsigned long long* grid, unsigned long long* slab) {
     std::memset(&g, 0, sizeof g);
@@ -1268,7 +1350,13 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
     L.off_shg = al(L.off_shcull + (L.has_shcull ? sizeof(DevShadowCull) * (size_t)n_lights * (size_t)n_spheres : 0));
     L.off_shgrid = al(L.off_shg + (L.has_shg ? sizeof(DevShadowGrid) * (size_t)n_lights : 0));
     L.off_shslab = al(L.off_shgrid + (L.has_shg ? sizeof(unsigned long long) * SHGRID_N * SHGRID_N * (size_t)n_lights : 0));
-    L.bytes = al(L.off_shslab + (L.has_shg ? sizeof(unsigned long long) * (SHGRID_SLABS + 2) * (size_t)n_lights : 0)) + 256;
+    L.off_clus = al(L.off_shslab + (L.has_shg ? sizeof(unsigned long long) * (SHGRID_SLABS + 2) * (size_t)n_lights : 0));
+    // per-lane cluster pre-cull of the bundle kernel's trace bundles (CULL_MIN_SPHERES <= S <= 64);
+    // RT_TRACE_CLUSTERS=0 turns it off, =2..16 sets the cluster size (A/B)
+    int csize = CLUSTER_SIZE;
+    if (const char* cv = std::getenv("RT_TRACE_CLUSTERS")) csize = std::atoi(cv);
+    const bool want_clus = n_spheres >= CULL_MIN_SPHERES && n_spheres <= 64 && csize >= 1;
+    L.bytes = al(L.off_clus + (want_clus ? sizeof(DevCluster) * MAX_CLUSTERS : 0)) + 256;
 
     std::vector<unsigned char> blob(L.bytes, 0);
     DevSphere* sph = (DevSphere*)(blob.data() + L.off_sph);
@@ -1335,6 +1423,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
             build_shadow_grid(li[j], frames[(size_t)j], sph, cull, n_spheres, ((DevShadowGrid*)(blob.data() + L.off_shg))[j],
                               (unsigned long long*)(blob.data() + L.off_shgrid) + (size_t)j * SHGRID_N * SHGRID_N,
                               (unsigned long long*)(blob.data() + L.off_shslab) + (size_t)j * (SHGRID_SLABS + 2));
+    if (want_clus) L.n_clus = build_clusters(cull, n_spheres, csize, (DevCluster*)(blob.data() + L.off_clus));
     if (L.has_shcull) {  // sphere centres in each light's shadow-cull frame (culling only)
         DevShadowCull* sc = (DevShadowCull*)(blob.data() + L.off_shcull);
         for (int j = 0; j < n_lights; ++j)
@@ -2150,7 +2239,8 @@ int rt_dispatch_order(rt_ctx* ctx, int* out_order) {
     // (a new scene or frame size is measured again from its first single-frame launch)
     if (ctx->dev.empty()) return fail(ctx, RT_ERR_INVALID_ARG, "context without a device");
     const Device::OrderTuner& t = ctx->dev[0].order;
-    const bool fresh = t.scene_gen == ctx->scene_gen && ctx->view_ok && t.W == ctx->view_w && t.H == ctx->view_h;
+    // (the tuner measures single-frame launches of view_w x view_rows traced rows, whatever the view height)
+    const bool fresh = t.scene_gen == ctx->scene_gen && ctx->view_ok && t.W == ctx->view_w && t.H == ctx->view_rows;
     *out_order = ctx->order_fixed >= 0 ? ctx->order_fixed : fresh ? ctx->dev[0].order.chosen : -1;
     return RT_OK;
 }

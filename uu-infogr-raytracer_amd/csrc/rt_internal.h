@@ -63,6 +63,20 @@ struct DevSphereCull {
     float cx, cy, cz, rr;
 };
 
+// Sphere clusters of the bundle kernel's per-lane pre-cull (CULL_MIN_SPHERES <= S <= 64; culling only): a
+// bounding sphere (centre, radius R >= |c_i - centre| + r'_i of every member, r' as in DevSphereCull) and
+// the member set as a mask over sphere indices.  A trace bundle whose cone allows no culling (the reflected
+// segments deep in mirror chains, where a wave's rays fan out) tests each lane's own ray against the
+// clusters and takes the union of the kept clusters' members (rt_kernel.hip cluster_mask) instead of every
+// sphere.  Built on the host by median splits of the centres (rt_api.cpp build_clusters).
+struct DevCluster {
+    float cx, cy, cz, R;
+    unsigned long long members;
+    unsigned long long pad;
+};
+constexpr int CLUSTER_SIZE = 4;   // spheres per cluster (tools/trace_cull_model.py: 2 and 4 alike, 8 worse)
+constexpr int MAX_CLUSTERS = 32;
+
 // Per-(light, sphere) shadow-cull record (culling only): the sphere centre in the light's frame
 // (C.U, C.V, C.A, rounded from double) and r' + 2^-18 |C| (the projection-error allowance,
 // rt_kernel.hip shadow_sphere_cull).  [L][S], built when L * S <= SHADOW_CULL_MAX_ENTRIES (larger
@@ -153,10 +167,12 @@ struct LaunchParams {
     const DevShadowGrid* shg;     // [L] or NULL (no shadow grid: the per-level bound instead)
     const unsigned long long* shgrid;  // [L][SHGRID_N^2]
     const unsigned long long* shslab;  // [L][SHGRID_SLABS + 2]
+    const DevCluster* clus;            // [n_clus] (n_clus 0: no per-lane pre-cull)
     const float* lxt;  // [W]: ((float)x / W - 0.5f) * pw, TracePixel :963-965
     const float* lyt;  // [H]: ((float)y / H - 0.5f) * ph
     int S, P, L, limit;
     int lights_a2_ok;  // every light's 2a = 2 p.p is finite and > 0 (the shadow loops' exact-threshold form)
+    int n_clus;
     // view, RayTracer.cs:511-523 and :892-896 (computed on the host)
     float cam[3], right[3], up[3], fwd[3];
     float pw, ph, nearc;

@@ -1052,6 +1052,42 @@ __device__ __forceinline__ unsigned long long cull_mask(const LaunchParams& p, c
     return __builtin_amdgcn_ballot_w64(in && !cull);
 }
 
+// Per-lane cluster pre-cull (p.n_clus > 0) for a trace bundle that allows no culling -- the reflected segments
+// deep in mirror chains, where a wave's rays fan out into a cone of 0.5 or wider and the bundle would test
+// every sphere (tools/trace_cull_model.py: such bundles hold 6.6 of the 7.3 sphere candidates a C4 wave tests
+// on its reflected segments, while 1-3 spheres are reachable).  Each lane tests its own ray against the
+// clusters' bounding spheres (DevCluster: R >= |c_i - Cc| + r'_i for every member) and the wave takes the
+// union of the kept clusters' members.  Converged call (idle lanes carry a copy of an active lane's ray).
+// Exactness (culling only, FMA allowed): cull_mask's rules for one ray (R = 0, delta = 0) applied to the
+// bounding sphere -- the line misses it by the margin 2^-8 (|w|_1 + R), w = Cc - o, or its centre lies behind
+// the origin by R plus that margin.  Then for every member i the line-to-centre distance exceeds
+// r'_i + 2^-8 (|c_i - o| + 0) (|c_i - o| <= |w| + R) or its centre is behind by more than the margin: the
+// conditions under which cull_mask drops sphere i for this lane, which make its IntersectsSphere distance
+// non-selectable.  The perpendicular distance is |w x A| (no cancellation), A = d / |d| by the hardware rsq
+// (~1 ulp, far inside the margin); the products are fused (culling-only arithmetic: fewer roundings).  A lane whose a = d.d is outside [0.5, 2] or whose origin is not finite
+// keeps every cluster, and a cluster with a NaN R (a member without a usable cull record) is never culled.
+__device__ __forceinline__ unsigned long long cluster_mask(const LaunchParams& p, f3 o, f3 d) {
+    const float a = dot(d, d);
+    const f3 A = cnormalize(d);
+    const float ol = __builtin_fabsf(o.x) + __builtin_fabsf(o.y) + __builtin_fabsf(o.z);
+    const bool ok = a >= 0.5f && a <= 2.0f && ol < 0x1p40f;
+    unsigned long long m = 0;
+    for (int j = 0; j < p.n_clus; ++j) {  // wave-uniform
+        const DevCluster c = p.clus[j];
+        const f3 w = sub(mk(c.cx, c.cy, c.cz), o);
+        const float dc = (__builtin_fabsf(w.x) + __builtin_fabsf(w.y) + __builtin_fabsf(w.z)) * (1.0f + 0x1p-20f);
+        const float mgn = 0x1p-8f * (dc + c.R);
+        const f3 x = mk(__builtin_fmaf(w.y, A.z, -(w.z * A.y)), __builtin_fmaf(w.z, A.x, -(w.x * A.z)),
+                        __builtin_fmaf(w.x, A.y, -(w.y * A.x)));  // w x A
+        const float T = c.R + mgn;
+        const bool line = __builtin_fmaf(x.z, x.z, __builtin_fmaf(x.y, x.y, x.x * x.x)) > T * T;
+        const bool behind = -__builtin_fmaf(w.z, A.z, __builtin_fmaf(w.y, A.y, w.x * A.x)) - c.R > mgn;
+        const bool valid = dc >= 0x1p-30f && dc < 0x1p40f;
+        if (__builtin_amdgcn_ballot_w64(!(ok && valid && (line || behind))) != 0) m |= c.members;  // NaN: kept
+    }
+    return m;
+}
+
 // Shadow bundles.  Every shadow ray of light l has the same direction p_l (the light
 // POSITION, Q2), so a sphere can block lane k only if the line {hp_k + s p_l} passes within
 // r of its centre: a 2-D test in the light's frame (U, V, A ~ p_l/|p_l|, host-built).  One bound
@@ -1196,7 +1232,9 @@ __device__ __forceinline__ Hit nearest_bundle(const LaunchParams& p, f3 o, f3 d,
         // origins) takes every sphere without the per-lane cull arithmetic, whose ballot would keep every
         // sphere anyway (C4 -0.7 %, C5 -0.6 %, profiles/ab/r04_nocull_ab.txt; culling wider cones than 0.25
         // less eagerly measured +2 %).  Wave-uniform.
-        unsigned long long m = use_box ? pmask : !B.ok ? (n == 64 ? ~0ull : (1ull << n) - 1ull) : cull_mask(p, B, base, n);
+        // A cone too wide for the bundle cull: the per-lane cluster pre-cull when the scene has clusters (S <= 64).
+        const unsigned long long all = n == 64 ? ~0ull : (1ull << n) - 1ull;
+        unsigned long long m = use_box ? pmask : B.ok ? cull_mask(p, B, base, n) : p.n_clus ? cluster_mask(p, o, d) & all : all;
         // candidates in ascending order, selection by selects (take_*, no per-lane branches); the
         // root sequence is chosen once per wave (2a finite-positive on every lane: the usual case)
         if (__builtin_amdgcn_ballot_w64(!a2_ok) == 0)
