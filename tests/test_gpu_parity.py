@@ -161,6 +161,31 @@ def test_trace_cluster_precull_vs_oracle(gpu_ctx, oracle, seed, monkeypatch):
         assert ray_counts(st) == ray_counts(ost)
 
 
+POW_EXPONENTS = [3.7, 7.25, 12.0, float.fromhex("0x1.946b02p+4"), float.fromhex("0x1.273c82p+2"), 2.486319, 21.299271, 60.566631, 9.88111, 0.75, 1.5,
+                 33.0, 0.1, 5.0e-3, 63.9]
+
+
+@pytest.mark.parametrize("k", list(range(len(POW_EXPONENTS))))
+def test_generic_specular_exponents_vs_oracle(gpu_ctx, oracle, k):
+    """Specular exponents other than 0.5, 1, 2 (Math.Pow, RayTracer.cs:691): the kernels run the restatement of
+    glibc's pow (csrc/rt_pow.h), the oracle the host's glibc pow.  Metal and Plastic spheres with the exponent,
+    among them the two at which the device's own pow and glibc round to different floats (profiles/r06_pow_check.txt),
+    on the direct kernel (C3's 8 spheres) and the bundle kernel (C4's 64): every pixel the oracle's."""
+    n = float(np.float32(POW_EXPONENTS[k]))
+    for cid, size in (("C3", (480, 270)), ("C4", (384, 216))):
+        base = scenes.config(cid)
+        sph = [scenes.Sphere(s.center, s.radius, (scenes.Material.metal if i % 2 else scenes.Material.plastic)(
+            s.material.kd if any(s.material.kd) else (0.7, 0.6, 0.5), n)) if i % 3 != 2 else s
+               for i, s in enumerate(base.spheres)]
+        pl = [scenes.Plane(p.center, p.normal, scenes.Material.metal((0.8, 0.8, 0.8), n)) for p in base.planes]
+        sc = scenes.Scene(f"{cid}_pow{k}", size[0], size[1], sph, pl, base.lights, base.ambient, base.recursion_limit,
+                          base.camera)
+        px, st = render_gpu(gpu_ctx, sc)
+        want, ost = oracle.render(sc, oracle.MODE_NEAREST, 8)
+        assert_same(px, want, f"{sc.name} n={n!r}")
+        assert ray_counts(st) == ray_counts(ost)
+
+
 @pytest.mark.parametrize("n_lights", [3000, 4200])
 def test_many_lights_with_and_without_the_shadow_cull_table(gpu_ctx, oracle, n_lights):
     """The bundle kernel's shadow culling reads the sphere centres pre-projected into each light's
@@ -430,8 +455,10 @@ def test_view_height_cut_frames_are_the_full_frames_rows(oracle, monkeypatch, ci
             for _ in range(2 if order is not None else 1):
                 assert_same(ctx.render(W, Hc).copy(), want[:Hc], f"{cid} rt_render {W}x{Hc} of {W}x{VH}")
             out = torch.zeros(W * Hc, dtype=torch.int32, device="cuda")
-            for _ in range(60 if order is None else 2):  # (None: past the tuner's probes and its recording)
+            for k in range(60 if order is None else 2):  # (None: past the tuner's probes and its recording)
                 ctx.render_device(W, Hc, out.data_ptr(), st)
+                if k % 10 == 9:  # (the tuner reads its probes' events as they complete)
+                    torch.cuda.synchronize()
             torch.cuda.synchronize()
             assert_same(out.cpu().numpy().reshape(Hc, W), want[:Hc], f"{cid} rt_render_device {W}x{Hc}")
             # the tuner's choice reads as made (the bundle kernel's cut frames are single-frame launches too; the

@@ -44,5 +44,23 @@ c)  # the device's f64 pow against glibc (tools/pow_check.hip, built on the CPU 
         -- python3 $R/tools/tick_deep_probe.py deep --variants bench --runs 4 > $O/tick_trace.log 2>&1 || { tail $O/tick_trace.log; exit 1; }
     cat $O/tick_trace.log
     ;;
+d)  # the GPU suite (generic exponents, clusters of 8), the restated pow on the device, the deep Tick under the
+    # slow-call probe build (tools/probes/slow_calls.patch: HIP calls and trace launches over 300 us on stderr)
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_d.log 2>&1 \
+        || { echo "GPU TESTS FAILED"; tail -30 $O/gpu_d.log; exit 1; }
+    echo "gpu tests: $(tail -1 $O/gpu_d.log)"
+    timeout -k 10 600 ./tools/pow_check > $O/pow_check_d.txt 2>&1; rc=$?; tail -8 $O/pow_check_d.txt; [ $rc -le 1 ] || exit 1
+    timeout -k 10 300 python -u tools/tick_deep_probe.py deep --variants bench touched --runs 6 \
+        --lib uu-infogr-raytracer_amd/lib/probe/libraytracer_hip_slowcalls.so > $O/tick_slow.txt 2>&1 || { tail $O/tick_slow.txt; exit 1; }
+    grep -v amdgpu.ids $O/tick_slow.txt | tail -40
+    ;;
+e)  # deep-Tick stall: frames-in-flight bound (RT_TICK_INFLIGHT 0 = none, 2, 3, 4, 8) and the copy-slice mode, each
+    # after the bench's sequence, under the slow-call probe build (stderr: host calls over 300 us)
+    timeout -k 10 400 python -u tools/tick_deep_probe.py deep --variants bench --runs 4 --inflight 0 2 3 4 8 \
+        --lib uu-infogr-raytracer_amd/lib/probe/libraytracer_hip_slowcalls.so > $O/tick_inflight.txt 2>&1 || { tail $O/tick_inflight.txt; exit 1; }
+    timeout -k 10 200 python -u tools/tick_deep_probe.py deep --variants bench --runs 4 --modes slice \
+        --lib uu-infogr-raytracer_amd/lib/probe/libraytracer_hip_slowcalls.so >> $O/tick_inflight.txt 2>&1 || { tail $O/tick_inflight.txt; exit 1; }
+    grep -v amdgpu.ids $O/tick_inflight.txt
+    ;;
 *)  echo "unknown step $1"; exit 2 ;;
 esac

@@ -22,6 +22,7 @@ sys.path.insert(0, os.path.join(ROOT, "uu-infogr-raytracer_amd"))
 
 
 def deep_runs(ctx, W, H, hosts, runs, label):
+    label = f"{label:18s}"
     n = len(hosts)
     for r in range(runs):
         calls = []
@@ -35,7 +36,7 @@ def deep_runs(ctx, W, H, hosts, runs, label):
         tw = time.perf_counter() - a
         dt = time.perf_counter() - t0
         top = sorted(range(n), key=lambda i: -calls[i])[:3]
-        print(f"{label:10s} run {r}: {n / dt:8.1f} fps  total {dt * 1e3:7.2f} ms  calls sum {sum(calls) * 1e3:6.2f} ms "
+        print(f"{label} run {r}: {n / dt:8.1f} fps  total {dt * 1e3:7.2f} ms  calls sum {sum(calls) * 1e3:6.2f} ms "
               f"(max {max(calls) * 1e6:7.1f} us at frames {top}: {[round(calls[i] * 1e6) for i in top]})  "
               f"wait {tw * 1e3:6.2f} ms", flush=True)
 
@@ -46,7 +47,10 @@ def deep(args):
     sc = scenes.config(args.config)
     W, H, n = sc.width, sc.height, 20
     torch.cuda.set_device(0)
-    for variant in args.variants:
+    for variant, inflight, mode in [(v, q, m) for m in args.modes for q in args.inflight for v in args.variants]:
+        os.environ["RT_TICK_INFLIGHT"] = str(inflight)  # (read at rt_create)
+        os.environ["RT_TICK_ASYNC"] = mode
+        label = f"{variant} q{inflight} {mode}"
         with Context(1) as ctx:
             ctx.set_scene(sc)
             ctx.set_counting(False)
@@ -72,8 +76,8 @@ def deep(args):
                 for hb in hosts:
                     ctx.render(W, H, hb)
             t = time.perf_counter()
-            deep_runs(ctx, W, H, hosts, args.runs, variant)
-            print(f"{variant:10s} ({(time.perf_counter() - t) * 1e3:.1f} ms for {args.runs} runs)", flush=True)
+            deep_runs(ctx, W, H, hosts, args.runs, label)
+            print(f"{label:10s} ({(time.perf_counter() - t) * 1e3:.1f} ms for {args.runs} runs)", flush=True)
             for hb in hosts:
                 ctx.unregister_host(hb)
 
@@ -115,7 +119,13 @@ def main():
     ap.add_argument("--configs", nargs="+", default=["C2", "C3"])
     ap.add_argument("--runs", type=int, default=6)
     ap.add_argument("--variants", nargs="+", default=["bench", "fresh", "touched"])
+    ap.add_argument("--lib", default="", help="library build to load instead of the in-tree one")
+    ap.add_argument("--inflight", nargs="+", type=int, default=[0], help="RT_TICK_INFLIGHT values (0: no bound)")
+    ap.add_argument("--modes", nargs="+", default=["stream"], help="RT_TICK_ASYNC values (stream: copy engine)")
     args = ap.parse_args()
+    if args.lib:
+        from raytracer_hip import abi
+        abi.LIB_PATH = os.path.abspath(args.lib)
     deep(args) if args.what == "deep" else chunks(args)
 
 

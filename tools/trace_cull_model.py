@@ -162,6 +162,8 @@ def main():
     CL = {z: clusters(C, np.sqrt(r2), z) for z in sizes}
     ccnt = np.zeros((L + 2, len(sizes), 4))  # per cluster size: union, union & bundle, clusters kept, cluster tests
     nok = np.zeros((L + 2, 2 + len(sizes)))  # bundles that allow no culling (cone >= 0.5): count, reachable, union per z
+    thr = (8, 16, 24)
+    okb = np.zeros((len(thr), 3, len(sizes)))  # usable bundles with > thr candidates: count, candidates, & clusters
     for c0 in range(0, len(TX), 1024):
         xs = (TX[c0:c0 + 1024, None] * 8 + (lane & 7)[None]).ravel().astype(float)
         ys = (TY[c0:c0 + 1024, None] * 8 + (lane >> 3)[None]).ravel().astype(float)
@@ -189,6 +191,10 @@ def main():
                     ccnt[k, zi] += (um.sum(), (um & bm).sum(), kept, len(CL[z][2]))
                     if unusable:
                         nok[k, 2 + zi] += um.sum()
+                    else:
+                        for ti, tv in enumerate(thr):
+                            if bm.sum() > tv:
+                                okb[ti, :, zi] += (1, bm.sum(), (um & bm).sum())
     print(f"# {sc.name}: {len(TX)} sampled waves; per reflected segment k: waves with active lanes per sampled wave, "
           f"active lanes, bundle candidates, reachable spheres (per such wave)")
     for k in range(1, L + 2):
@@ -219,6 +225,11 @@ def main():
         print(f"  pre-cull on those bundles only, z={z} ({K} clusters): candidates {tn[0] * S / len(TX):.2f} -> "
               f"{tn[2 + zi] / len(TX):.2f} per sampled wave + {tn[0] * K / len(TX):.2f} cluster tests; "
               f"~{save / len(TX):.0f} VALU ops per wave saved (of ~2,075 per C4 wave, r05 PMC)")
+    for ti, tv in enumerate(thr):
+        print(f"  usable bundles with > {tv} candidates: {okb[ti, 0, 0] / len(TX):.3f} per sampled wave, "
+              f"{okb[ti, 1, 0] / len(TX):.2f} candidates -> & clusters " +
+              " / ".join(f"z={z}: {okb[ti, 2, zi] / len(TX):.2f} (+{okb[ti, 0, 0] * len(CL[z][2]) / len(TX):.2f} cluster tests)"
+                         for zi, z in enumerate(sizes)))
     for k0 in (2, 3, 4):  # pre-cull only from segment k0 on (a wave-uniform gate on the segment index)
         b = cnt[1:k0, 2].sum() + sum(ccnt[k0:, zi, 1].sum() for zi in [1])
         print(f"  pre-cull (z=8) from k={k0}: candidates {b / len(TX):.2f}, cluster tests {ccnt[k0:, 1, 3].sum() / len(TX):.2f}")

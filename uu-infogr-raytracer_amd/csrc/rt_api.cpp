@@ -151,6 +151,10 @@ struct Device {
     // rt_render_async's copy-engine hand-off (RT_TICK_ASYNC=stream): slot s traced -> copied events
     hipEvent_t ev_traced[2] = {}, ev_copied[2] = {};
     bool copy_pending[2] = {false, false};
+    // frames in flight of the copy-engine hand-off (rt_ctx::tick_inflight): frame f's copy done -> ring[f % 16]
+    static constexpr int RING = 16;
+    hipEvent_t ev_ring[RING] = {};
+    uint64_t frames_issued = 0;
     float* d_view_tab = nullptr;  // lx[W] then ly[H] (view_tables)
     size_t view_tab_cap = 0;
     int tab_w = -1, tab_h = -1;
@@ -226,6 +230,7 @@ struct rt_ctx {
     bool counting = true;  // rt_set_counting: trace launches add to the ray counters
     uint64_t scene_gen = 0;  // rt_set_scene calls (the dispatch-order measurements belong to one scene)
     int order_fixed = -1;    // RT_DISPATCH_ORDER=0/1/2: that candidate for every single-frame launch
+    int tick_inflight = 0;   // rt_render_async: frames queued per worker before the host waits (0: no bound)
     int32_t* host_staging = nullptr;
     // host ranges registered through rt_register_host and their device-mapped addresses (one per
     // worker: each device writes its band set through its own mapping): only these are written by the
@@ -1045,6 +1050,8 @@ int rt_create_ex(int n_gpus, int flags, rt_ctx** out_ctx) {
     // RT_DISPATCH_ORDER=0/1/2 fixes the single-frame dispatch order (order_pick; A/B and tests)
     if (const char* o = std::getenv("RT_DISPATCH_ORDER"))
         if (o[0] >= '0' && o[0] < '0' + ORDER_CANDIDATES && o[1] == 0) ctx->order_fixed = o[0] - '0';
+    // RT_TICK_INFLIGHT=1..16 bounds rt_render_async's queued frames per worker (A/B)
+    if (const char* q = std::getenv("RT_TICK_INFLIGHT")) ctx->tick_inflight = std::max(0, std::min(16, std::atoi(q)));
     ctx->dev.resize((size_t)n_gpus);
     int cur = 0;
     (void)hipGetDevice(&cur);
@@ -1099,6 +1106,8 @@ void rt_destroy(rt_ctx* ctx) {
             if (d.ev_traced[i]) (void)hipEventDestroy(d.ev_traced[i]);
             if (d.ev_copied[i]) (void)hipEventDestroy(d.ev_copied[i]);
         }
+        for (hipEvent_t& ev : d.ev_ring)
+            if (ev) (void)hipEventDestroy(ev);
         if (d.copy_stream) (void)hipStreamDestroy(d.copy_stream);
         if (d.comm && g_rccl.CommDestroy) (void)g_rccl.CommDestroy(d.comm);
         if (d.d_scene) (void)hipFree(d.d_scene);
@@ -2091,6 +2100,10 @@ int rt_render_async(rt_ctx* ctx, int width, int height, int32_t* pixels) {
             }
             rc = flush_hand(ctx);  // (a slice-mode frame still pending)
             if (rc != RT_OK) return rc;
+            const uint64_t f = d.frames_issued++;
+            const int cap = ctx->tick_inflight;
+            if (cap > 0 && f >= (uint64_t)cap && d.ev_ring[(f - cap) % Device::RING])  // at most cap frames queued
+                HIP_TRY(ctx, hipEventSynchronize(d.ev_ring[(f - cap) % Device::RING]));
             if (d.copy_pending[slot]) HIP_TRY(ctx, hipStreamWaitEvent(d.async_stream, d.ev_copied[slot], 0));
             const bool pinned = mapped_host(ctx, g, pixels, frame_bytes) != nullptr;
             for (int c = 0; c < nc; ++c) {
@@ -2108,6 +2121,11 @@ int rt_render_async(rt_ctx* ctx, int width, int height, int32_t* pixels) {
                 if (rc != RT_OK) return rc;
             }
             HIP_TRY(ctx, hipEventRecord(d.ev_copied[slot], d.copy_stream));
+            if (cap > 0) {
+                hipEvent_t& er = d.ev_ring[f % Device::RING];
+                if (!er) HIP_TRY(ctx, hipEventCreateWithFlags(&er, hipEventDisableTiming));
+                HIP_TRY(ctx, hipEventRecord(er, d.copy_stream));
+            }
             d.copy_pending[slot] = true;
             d.async_next = slot ^ 1;
             continue;

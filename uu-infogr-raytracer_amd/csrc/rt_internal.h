@@ -74,7 +74,10 @@ struct DevCluster {
     unsigned long long members;
     unsigned long long pad;
 };
-constexpr int CLUSTER_SIZE = 4;   // spheres per cluster (tools/trace_cull_model.py: 2 and 4 alike, 8 worse)
+// Spheres per cluster: 4, 8 and 12 measured alike (C4 303.4-304.3 us, C5 1,114.7-1,116.3 us per frame against
+// 311.2-311.8 / 1,135-1,137 without clusters), 2 and 16 slower (profiles/ab/r06_clusters.txt); 8 tests the fewest
+// bounds.  (tools/trace_cull_model.py ranked 2 and 4 first: it prices a cluster test too cheaply.)
+constexpr int CLUSTER_SIZE = 8;
 constexpr int MAX_CLUSTERS = 32;
 
 // Per-(light, sphere) shadow-cull record (culling only): the sphere centre in the light's frame
