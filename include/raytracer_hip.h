@@ -327,20 +327,20 @@ int rt_comm_gather(rt_ctx* ctx, const void* d_send, size_t n_bytes, void* d_recv
                    void* hip_stream);
 
 /* ---- double-buffered frames ------------------------------ */
-/* Asynchronous Tick(): captures the current camera, enqueues the trace and returns at once;
- * rt_wait blocks until every enqueued frame is in its host buffer.  With two host buffers a
- * caller overlaps the trace of frame k+1 with its own use of frame k (the camera of k+1 can
- * already be set).  One in-order stream and two device frame buffers: frame k's D2H copy rides
- * in frame k+1's launch (a copy slice dispatched ahead of the trace workgroups, so the PCIe-bound
- * copy runs under the next trace) or is issued by rt_wait, rt_render, rt_unregister_host or
- * rt_destroy.  The slice writes only host buffers registered with rt_register_host (through their
- * device-mapped address); any other buffer gets hipMemcpyAsync on the same stream.  Measured on
- * MI355X at 1080p C2 (bench.py tick_*, median of 3 x 20 frames): a display loop two frames deep
- * (rt_wait per pair) 5.2-5.3k fps, 20 frames queued 5.4-5.5k fps, against 4.9-5.0k for the
- * synchronous rt_render; a trace stream plus a copy stream ordered by events (round 2) ran
- * 1.5-5.2k fps depending on the process (profiles/r03_tick_ab.txt).  n_gpus > 1: every worker
- * double-buffers its own band set on its own stream, and its hand-off rides in its next launch
- * (ABI 9; RT_CREATE_RCCL_GATHER contexts render synchronously here). */
+/* Asynchronous Tick(): captures the current camera, enqueues the trace and its hand-off into `pixels`
+ * and returns; rt_wait blocks until every enqueued frame is in its host buffer.  With two host buffers
+ * a caller overlaps the trace of frame k+1 with its own use of frame k (the camera of k+1 can already
+ * be set).  Each worker double-buffers its band set in device memory: frame k's copy into `pixels`
+ * runs on the copy engine on a second stream behind frame k's trace (registered `pixels`; a share
+ * under 0.5 Mpixel at n_gpus > 1 rides instead as a copy slice in frame k+1's trace launch, and an
+ * unregistered buffer gets the runtime's copies), while frame k+1 is traced.  At most 2 frames per
+ * worker are in flight: the call for frame k+2 first waits on the host for frame k's copy (deeper
+ * queues made the runtime block one copy call for 6-7 ms now and then, profiles/r06_tick_deep.txt;
+ * RT_TICK_INFLIGHT overrides).  Measured on one MI355X (bench.py tick_*, C3 1080p, median of 3 x 20
+ * frames): two frames deep with an rt_wait per pair 5.1-5.2k fps, 20 frames queued with one rt_wait
+ * 5.7-5.8k fps, against 4.8k for the synchronous rt_render.  n_gpus > 1: every worker double-buffers
+ * its own band set on its own streams and device (ABI 9; RT_CREATE_RCCL_GATHER contexts render
+ * synchronously here). */
 int rt_render_async(rt_ctx* ctx, int width, int height, int32_t* pixels);
 int rt_wait(rt_ctx* ctx);
 

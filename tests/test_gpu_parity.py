@@ -629,11 +629,18 @@ def _oracle_frame(oracle, W, H, cam):
     return oracle.render(s2, oracle.MODE_NEAREST, 4)[0]
 
 
-def test_render_async_deep_queue_one_wait(oracle):
+@pytest.mark.parametrize("inflight", [None, "0", "1", "3"])
+def test_render_async_deep_queue_one_wait(oracle, monkeypatch, inflight):
     """rt_render_async under load -- 9 frames queued with a new camera each, each into
     its own registered host buffer, and one rt_wait at the end; the frame size changes twice
-    mid-queue (reallocation of the device double buffer).  Frame k's copy rides in frame k+1's
-    launch (the copy slice), so a missing or misplaced ordering shows up as a wrong frame."""
+    mid-queue (reallocation of the device double buffer).  A missing or misplaced ordering between a
+    frame's trace, its hand-off and the next trace into the same device buffer shows up as a wrong
+    frame.  Under the default bound of 2 frames in flight (the call for frame k+2 waits for frame k's
+    copy), without a bound, and at 1 and 3 (RT_TICK_INFLIGHT, read at rt_create)."""
+    if inflight is None:
+        monkeypatch.delenv("RT_TICK_INFLIGHT", raising=False)
+    else:
+        monkeypatch.setenv("RT_TICK_INFLIGHT", inflight)
     sizes = [(96, 72)] * 4 + [(130, 66)] * 3 + [(33, 17), (96, 72)]
     cams = [((0.1 * k, 0.05 * k, -0.2 * k), 0.07 * k, -0.03 * k) for k in range(len(sizes))]
     bufs = [np.full(w * h, 0x7f7f7f7f, dtype=np.int32) for w, h in sizes]

@@ -212,6 +212,9 @@ struct SceneLayout {
 };
 }  // namespace
 
+// rt_render_async's frames in flight per worker behind the copy engine (rt_create_ex; RT_TICK_INFLIGHT)
+constexpr int TICK_INFLIGHT = 2;
+
 struct rt_ctx {
     int n_gpus = 1;            // band workers: devices, or streams on one device (RT_CREATE_SHARED_DEVICE)
     bool rccl_gather = false;  // RT_CREATE_RCCL_GATHER: rt_render gathers the bands to device 0 over RCCL, one D2H
@@ -1050,7 +1053,13 @@ int rt_create_ex(int n_gpus, int flags, rt_ctx** out_ctx) {
     // RT_DISPATCH_ORDER=0/1/2 fixes the single-frame dispatch order (order_pick; A/B and tests)
     if (const char* o = std::getenv("RT_DISPATCH_ORDER"))
         if (o[0] >= '0' && o[0] < '0' + ORDER_CANDIDATES && o[1] == 0) ctx->order_fixed = o[0] - '0';
-    // RT_TICK_INFLIGHT=1..16 bounds rt_render_async's queued frames per worker (A/B)
+    // rt_render_async keeps at most TICK_INFLIGHT frames per worker queued behind the copy engine: with more, one
+    // hipMemcpyAsync of the hand-off now and then blocked the host for 6-7 ms (the runtime, not the copy: 5.4-7.0 ms
+    // for an 8.3 MB copy that takes 160 us) -- a queued C3 run of 20 frames at 2.1-2.7k fps instead of 5.8k, in
+    // runs 0 and 2 of 4 unbounded, 1 of 4 at 4, every run at 8, none at 2 or 3 (profiles/r06_tick_deep.txt).  The
+    // double buffer needs no more than 2: frame k+2 is traced into frame k's buffer after frame k's copy anyway.
+    // RT_TICK_INFLIGHT=0..16 overrides (0: no bound; A/B)
+    ctx->tick_inflight = TICK_INFLIGHT;
     if (const char* q = std::getenv("RT_TICK_INFLIGHT")) ctx->tick_inflight = std::max(0, std::min(16, std::atoi(q)));
     ctx->dev.resize((size_t)n_gpus);
     int cur = 0;
