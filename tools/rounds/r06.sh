@@ -62,5 +62,19 @@ e)  # deep-Tick stall: frames-in-flight bound (RT_TICK_INFLIGHT 0 = none, 2, 3, 
         --lib uu-infogr-raytracer_amd/lib/probe/libraytracer_hip_slowcalls.so >> $O/tick_inflight.txt 2>&1 || { tail $O/tick_inflight.txt; exit 1; }
     grep -v amdgpu.ids $O/tick_inflight.txt
     ;;
+f)  # round-6 profiles of the final build: PMC passes + the bench line under a kernel trace, per config
+    # (tools/profile_round.sh -> gpurun_out/{pmc,trace}_<cfg>*, gpurun_out/pmc_traffic.json)
+    bash tools/profile_round.sh ${CONFIGS:-C3 C4 C5} || exit 1
+    for c in ${CONFIGS:-C3 C4 C5}; do echo "== $c"; cat gpurun_out/trace_${c}_reconcile.txt; grep -i "valu\|traffic" gpurun_out/pmc_${c}_summary.txt | head -8; done
+    ;;
+g)  # direct kernel A/B: both lights' shadow rays in one sphere loop (tools/ablate/r06_direct_merged2.patch, built
+    # to lib/probe/libraytracer_hip_merged2.so): parity subset under that build, then wall per frame against the product
+    RAYTRACER_HIP_LIB=$R/uu-infogr-raytracer_amd/lib/probe/libraytracer_hip_merged2.so timeout -k 10 600 python -u -m pytest \
+        tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread \
+        -k "full_size or random_scenes or camera_sweep or small_frames or generic_specular or recursion_limits or ragged" \
+        > $O/merged2_parity.log 2>&1 || { echo "PARITY FAILED"; tail -30 $O/merged2_parity.log; exit 1; }
+    echo "merged2 parity: $(tail -1 $O/merged2_parity.log)"
+    bash tools/ab_wall.sh "C3 C2" lib/probe/libraytracer_hip_merged2.so lib/libraytracer_hip.so | tee $O/merged2_wall.txt
+    ;;
 *)  echo "unknown step $1"; exit 2 ;;
 esac
