@@ -76,5 +76,19 @@ g)  # direct kernel A/B: both lights' shadow rays in one sphere loop (tools/abla
     echo "merged2 parity: $(tail -1 $O/merged2_parity.log)"
     bash tools/ab_wall.sh "C3 C2" lib/probe/libraytracer_hip_merged2.so lib/libraytracer_hip.so | tee $O/merged2_wall.txt
     ;;
+h)  # N > 1 rehearsals of the final build on one GPU (gloo ranks sharing it; timings not results): the GPU paths'
+    # rehearsal tests, then the driver's scaling shape at N = 3 / 8 with rank 0's measured share, frames verified
+    timeout -k 10 400 python -u -m pytest tests/test_gpu_paths.py -x -q --timeout 120 --timeout-method thread -k "rehearsal" \
+        > $O/rehearsal_tests.log 2>&1 || { echo "REHEARSAL TESTS FAILED"; tail -40 $O/rehearsal_tests.log; exit 1; }
+    echo "rehearsal tests: $(tail -1 $O/rehearsal_tests.log)"
+    for n in 3 8; do
+      timeout -k 10 300 python bench.py --gpus $n --rehearse-gloo --steps 20 --warmup 5 --no-cpu-baseline --no-tick \
+          --master-port $((29700 + n)) --verify > $O/rehearse$n.json 2> $O/rehearse$n.err || { tail -20 $O/rehearse$n.err; exit 1; }
+      python3 -c "
+import json; d = json.loads(open('$O/rehearse$n.json').read().strip().splitlines()[-1])
+print('N=$n', d['config']['workload'][:3], 'verified', d.get('verified_frames'), d['config']['parallelism'][:160])
+for k, v in d.get('also', {}).items(): print('   also', k, 'verified', v.get('verified_frames'), v['config'].get('rank0_tail_rows'))"
+    done
+    ;;
 *)  echo "unknown step $1"; exit 2 ;;
 esac
