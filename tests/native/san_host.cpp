@@ -542,6 +542,100 @@ void check_cluster_cull() {
     std::printf("cluster_cull: %ld of %ld (ray, cluster) tests culled, every member checked\n", culled, tests);
 }
 
+// The direct kernel's per-lane shadow pre-test (rt_kernel.hip shadow_pre_lane / shadow_pre_keep, restated in
+// binary32 with the same fmas; records from rt_set_scene's build_shadow_pre): random scenes of 1-11 spheres with
+// ordinary, grazing, tiny and huge lights, tiny / NaN / far spheres, and hit points on and near sphere surfaces,
+// on shadow lines grazing a sphere, anywhere, far away and non-finite.  For every (lane, light, sphere) the
+// pre-test drops, the oracle's binary32 IntersectShadowLight test (epsilon 0.001) must find no collision.
+bool pre_keeps(const DevLight& l, const DevShadowCull& e, rt_vec3 hp) {
+    const float ou = std::fmaf(hp.z, l.uz, std::fmaf(hp.y, l.uy, hp.x * l.ux));
+    const float ov = std::fmaf(hp.z, l.vz, std::fmaf(hp.y, l.vy, hp.x * l.vx));
+    const float oa = std::fmaf(hp.z, l.az, std::fmaf(hp.y, l.ay, hp.x * l.ax));
+    const float l1 = std::fabs(ou) + std::fabs(ov) + std::fabs(oa);
+    const float ml = l1 < 0x1p38f ? std::fmaf(l1, 0x1.01p-8f, 0x1p-30f) : INFINITY;
+    const float wu = e.cu - ou, wv = e.cv - ov;
+    const float T = e.rr + ml;
+    const bool line = std::fmaf(wu, wu, wv * wv) > T * T;
+    const bool behind = oa - e.ca > ml;
+    return !(line || behind);
+}
+
+void check_shadow_pre() {
+    long culled = 0, pairs = 0;
+    for (int it = 0; it < 60; ++it) {
+        const float scale = it % 4 == 3 ? 1000.0f : it % 4 == 2 ? 30.0f : it % 8 == 1 ? 1e-3f : 1.0f;
+        const int S = 1 + (int)(next64() % (CULL_MIN_SPHERES - 1)), L = 1 + (int)(next64() % 4);
+        std::vector<rt_sphere> sph((size_t)S);
+        std::vector<rt_light> li((size_t)L);
+        for (rt_sphere& q : sph) {
+            q.center = v3(unif(-8, 8) * scale, unif(-1, 3) * scale, unif(2, 40) * scale);
+            q.radius = unif(0.05f, 1.5f) * scale;
+            q.material = material((int)(next64() % 5));
+        }
+        if (S > 1 && it % 5 == 1) sph[1].radius = 1e-25f;            // r'^2 below the cull's floor: never dropped
+        if (S > 2 && it % 6 == 2) sph[2].radius = NAN;
+        if (S > 3 && it % 7 == 3) sph[3].center = v3(3e11f, 0, 0);   // |C_f|_1 >= 2^38: never dropped
+        for (int j = 0; j < L; ++j) {
+            rt_light& l = li[(size_t)j];
+            l.position = v3(unif(-40, 40), unif(-5, 20), unif(-20, 40));
+            l.intensity = 1.0f;
+            if (j == 1 && it % 3 == 0) l.position = v3(unif(-40, 40), 1e-3f, unif(-1, 1));  // grazing
+            if (j == 2 && it % 4 == 0) l.position = v3(1e-30f, 0, 0);                      // a below 2^-40
+            if (j == 3 && it % 2 == 0) l.position = v3(0, 3e4f, 0);
+            if (j == 0 && it % 9 == 4) l.position = v3(0, 0, 0);                           // 2a = 0: literal path
+        }
+        rt_ctx ctx;
+        CHECK(rt_set_scene(&ctx, sph.data(), S, nullptr, 0, li.data(), L, v3(0.1f, 0.1f, 0.1f), 3) == RT_OK, "scene");
+        const SceneLayout& lay = ctx.layout;
+        CHECK(lay.has_shpre, "pre-test records for S = %d", S);
+        if (!lay.has_shpre) continue;
+        const int s_pad = S + (S & 1);
+        const DevShadowCull* pre = (const DevShadowCull*)(lay.host_blob.data() + lay.off_shpre);
+        const DevLight* dl = (const DevLight*)(lay.host_blob.data() + lay.off_li);
+        for (int j = 0; j < L; ++j) {
+            const DevLight& l = dl[j];
+            if (S & 1) CHECK(std::isinf(pre[(size_t)j * s_pad + S].cu), "padding record dropped");
+            const double U[3] = {l.ux, l.uy, l.uz}, V[3] = {l.vx, l.vy, l.vz}, A[3] = {l.ax, l.ay, l.az};
+            for (int k = 0; k < 4000; ++k) {
+                rt_vec3 hp;
+                const rt_sphere& s = sph[next64() % (size_t)S];
+                const int kind = k % 5;
+                if (kind == 0) {
+                    hp = v3(unif(-20, 20) * scale, unif(-3, 6) * scale, unif(-5, 60) * scale);
+                } else if (kind == 1) {  // on / just off a sphere's surface
+                    const double d[3] = {unif(-1, 1), unif(-1, 1), unif(-1, 1)};
+                    const double n = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]) + 1e-30;
+                    const double r = (double)s.radius * (1.0 + unif(-1e-3f, 1e-2f));
+                    hp = v3((float)(s.center.x + r * d[0] / n), (float)(s.center.y + r * d[1] / n),
+                            (float)(s.center.z + r * d[2] / n));
+                } else if (kind == 2 || kind == 3) {  // a shadow line grazing a sphere
+                    const double ang = unif(0, 6.2831853f), rr = (double)s.radius * (1.0 + unif(-2e-3f, 2e-2f));
+                    const double ax = unif(-30, 10) * scale;
+                    double q[3];
+                    const double c[3] = {s.center.x, s.center.y, s.center.z};
+                    for (int e = 0; e < 3; ++e) q[e] = c[e] + rr * (std::cos(ang) * U[e] + std::sin(ang) * V[e]) + ax * A[e];
+                    hp = v3((float)q[0], (float)q[1], (float)q[2]);
+                } else {  // far away, and non-finite
+                    const float f = std::ldexp(1.0f, (int)(next64() % 40));
+                    hp = v3(unif(-20, 20) * scale * f, unif(-3, 6) * scale, unif(-5, 60) * scale * f);
+                    if (k % 97 == 4) hp.x = NAN;
+                    if (k % 89 == 9) hp.z = INFINITY;
+                }
+                for (int i = 0; i < S; ++i) {
+                    ++pairs;
+                    if (pre_keeps(l, pre[(size_t)j * s_pad + i], hp)) continue;
+                    ++culled;
+                    int col = 0;
+                    oracle_intersect_sphere(hp, li[(size_t)j].position, sph[(size_t)i].center, sph[(size_t)i].radius,
+                                            0.001f, &col);
+                    CHECK(!col, "scene %d light %d: sphere %d dropped but blocks hp (%a, %a, %a)", it, j, i, hp.x, hp.y, hp.z);
+                }
+            }
+        }
+    }
+    std::printf("shadow_pre: %ld of %ld (lane, light, sphere) triples dropped, each checked unblocked\n", culled, pairs);
+}
+
 // Single-frame row order (row_order): a floor below the camera fills the bottom rows (high y), so they
 // are dispatched first; a ceiling above it puts the top rows first; with no plane and no sphere every
 // row costs the same and the order stays natural.
@@ -676,6 +770,7 @@ int main() {
     check_shadow_threshold();
     check_tiles_by_cost();
     check_shadow_grid();
+    check_shadow_pre();
     check_ball_cull();
     check_cluster_cull();
     check_row_order();

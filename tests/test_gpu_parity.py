@@ -150,7 +150,7 @@ def test_shadow_grid_scenes_vs_oracle(gpu_ctx, oracle, seed, monkeypatch):
 def test_trace_cluster_precull_vs_oracle(gpu_ctx, oracle, seed, monkeypatch):
     """The bundle kernel's per-lane cluster pre-cull of trace bundles too wide for the bundle cull (rt_kernel.hip
     cluster_mask; clusters of RT_TRACE_CLUSTERS spheres built at rt_set_scene, 0 = off): the mirror-heavy grid
-    scenes at unit, 30x and 1000x scale, clusters of 2, 4 (the default) and 8 spheres and none -- every pixel
+    scenes at unit, 30x and 1000x scale, clusters of 4, 2 and 8 (the default) spheres and none -- every pixel
     and ray count the oracle's."""
     sc = shadow_grid_scene(1000 + seed, 128, 80)
     want, ost = oracle.render(sc, oracle.MODE_NEAREST, 8)
@@ -158,6 +158,53 @@ def test_trace_cluster_precull_vs_oracle(gpu_ctx, oracle, seed, monkeypatch):
         monkeypatch.setenv("RT_TRACE_CLUSTERS", z)
         px, st = render_gpu(gpu_ctx, sc)
         assert_same(px, want, f"{sc.name} RT_TRACE_CLUSTERS={z}")
+        assert ray_counts(st) == ray_counts(ost)
+
+
+def shadow_pre_scene(seed, width=160, height=96):
+    """A C2/C3-like scene for the direct kernel's per-lane shadow pre-test (1-11 spheres, 1-4 lights): diffuse,
+    plastic and mirror spheres at 1e-3x, unit, 30x and 1000x scale, lights that graze the floor, sit at the
+    origin (2a = 0: the literal root formula, no pre-test), have a = p.p below 2^-40 (no culling) or lie far out,
+    a tiny sphere and one far from the others, a checkered floor and cameras anywhere in the scene."""
+    rng = np.random.default_rng(30_000 + seed)
+    scale = [1.0, 30.0, 1000.0, 1e-3][seed % 4]
+    f = lambda x: float(np.float32(x))  # noqa: E731
+    ns = int(rng.integers(1, 12))
+    mats = [scenes.Material.mirror(scenes.ONE), scenes.Material.diffuse((0.8, 0.3, 0.2)),
+            scenes.Material.plastic((0.2, 0.7, 0.3), 1.0), scenes.Material.diffuse_mirror((0.6, 0.6, 0.9), (0.5,) * 3),
+            scenes.Material.plastic((0.9, 0.9, 0.2), 0.5)]
+    sph = [scenes.Sphere((f(rng.uniform(-6, 6) * scale), f(rng.uniform(-0.7, 1.5) * scale), f(rng.uniform(3, 20) * scale)),
+                         f(rng.uniform(0.3, 1.5) * scale), mats[int(rng.integers(0, 5))]) for _ in range(ns)]
+    if seed % 5 == 1 and ns > 1:
+        sph[1] = scenes.Sphere(sph[1].center, f(1e-3 * scale), mats[1])  # tiny
+    if seed % 7 == 3 and ns > 2:
+        sph[2] = scenes.Sphere((f(4e4 * scale), 0.0, f(9 * scale)), f(scale), mats[2])  # far from the others
+    planes = [scenes.Plane((0.0, f(-1 * scale), 0.0), (0.0, 1.0, 0.0), scenes.REF_PLANES[0].material)]
+    nl = int(rng.integers(1, 5))
+    lights = [scenes.Light((f(rng.uniform(-30, 30) * scale), f(rng.uniform(0.5, 12) * scale),
+                            f(rng.uniform(-10, 30) * scale)), 1.0) for _ in range(nl)]
+    if seed % 3 == 0:
+        lights[0] = scenes.Light((f(25 * scale), f(1e-3 * scale), f(8 * scale)), 1.0)  # grazing
+    if seed % 6 == 1:
+        lights[-1] = scenes.Light((0.0, 0.0, 0.0), 0.7)  # 2a = 0
+    if seed % 8 == 5:
+        lights[-1] = scenes.Light((f(1e-25), 0.0, 0.0), 0.7)  # a < 2^-40
+    cam = ((f(rng.uniform(-2, 2) * scale), f(rng.uniform(-0.5, 2) * scale), f(rng.uniform(-4, 2) * scale)),
+           f(rng.uniform(-0.6, 0.6)), f(rng.uniform(-0.3, 0.4)))
+    return scenes.Scene(f"pre{seed}", width, height, sph, planes, lights, scenes.REF_AMBIENT,
+                        int(rng.choice([0, 1, 2, 4])), cam)
+
+
+@pytest.mark.parametrize("seed", list(range(32)))
+def test_direct_shadow_pretest_vs_oracle(gpu_ctx, oracle, seed, monkeypatch):
+    """The direct kernel's per-lane shadow pre-test (rt_kernel.hip shadow_pre_keep, records built at
+    rt_set_scene; RT_SHADOW_PRE=0 = every sphere tested): both give the oracle's pixels and ray counts."""
+    sc = shadow_pre_scene(seed)
+    want, ost = oracle.render(sc, oracle.MODE_NEAREST, 8)
+    for pre in ("1", "0"):
+        monkeypatch.setenv("RT_SHADOW_PRE", pre)
+        px, st = render_gpu(gpu_ctx, sc)
+        assert_same(px, want, f"{sc.name} RT_SHADOW_PRE={pre}")
         assert ray_counts(st) == ray_counts(ost)
 
 

@@ -90,5 +90,25 @@ print('N=$n', d['config']['workload'][:3], 'verified', d.get('verified_frames'),
 for k, v in d.get('also', {}).items(): print('   also', k, 'verified', v.get('verified_frames'), v['config'].get('rank0_tail_rows'))"
     done
     ;;
+i)  # generic A/B of probe builds: LIBS="name ..." (lib/probe/libraytracer_hip_<name>.so), CFGS="C3 C2 ...": the parity
+    # subset under each build, then wall per frame against the product (tools/ab_wall.sh, two interleaved passes)
+    args=""
+    for n in $LIBS; do
+        RAYTRACER_HIP_LIB=$R/uu-infogr-raytracer_amd/lib/probe/libraytracer_hip_$n.so timeout -k 10 600 python -u -m pytest \
+            tests/test_gpu_parity.py -m gpu -x -q --timeout 120 --timeout-method thread \
+            -k "full_size or random_scenes or camera_sweep or small_frames or generic_specular or recursion_limits or ragged or shadow_grid or cluster or bundle_light_counts or many_lights" \
+            > $O/${n}_parity.log 2>&1 || { echo "PARITY FAILED $n"; tail -30 $O/${n}_parity.log; exit 1; }
+        echo "$n parity: $(tail -1 $O/${n}_parity.log)"
+        args="$args lib/probe/libraytracer_hip_$n.so"
+    done
+    bash tools/ab_wall.sh "$CFGS" $args lib/libraytracer_hip.so | tee $O/ab_${TAG:-i}.txt
+    ;;
+j)  # the GPU suite on the product (direct kernel's shadow pre-test), then wall per frame against the build without
+    # it (lib/probe/libraytracer_hip_nopre.so: tools/ablate/r06_direct_shadow_pre_revert.patch)
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_j.log 2>&1 \
+        || { echo "GPU TESTS FAILED"; tail -30 $O/gpu_j.log; exit 1; }
+    echo "gpu tests: $(tail -1 $O/gpu_j.log)"
+    bash tools/ab_wall.sh "${CFGS:-C3 C2 C1 REF}" lib/probe/libraytracer_hip_nopre.so lib/libraytracer_hip.so | tee $O/ab_pre_product.txt
+    ;;
 *)  echo "unknown step $1"; exit 2 ;;
 esac

@@ -200,7 +200,8 @@ struct Device {
 struct SceneLayout {
     int S = 0, P = 0, L = 0, limit = 0;
     size_t off_sph = 0, off_mat = 0, off_pl = 0, off_li = 0, off_cull = 0, off_shcull = 0, bytes = 0;
-    size_t off_shg = 0, off_shgrid = 0, off_shslab = 0, off_clus = 0;
+    size_t off_shg = 0, off_shgrid = 0, off_shslab = 0, off_clus = 0, off_shpre = 0;
+    bool has_shpre = false;  // the direct kernel's shadow pre-test records (DevShadowCull [L][S + (S & 1)])
     int n_clus = 0;  // DevCluster records (the bundle kernel's per-lane pre-cull), 0: none
     bool has_shcull = false;
     bool has_shg = false;  // per-light shadow grids (DevShadowGrid) for the merged shadow pass
@@ -557,6 +558,7 @@ void scene_params(const rt_ctx* ctx, const Device& d, LaunchParams& lp) {
     lp.shgrid = L.has_shg ? (const unsigned long long*)(base + L.off_shgrid) : nullptr;
     lp.shslab = L.has_shg ? (const unsigned long long*)(base + L.off_shslab) : nullptr;
     lp.clus = L.n_clus ? (const DevCluster*)(base + L.off_clus) : nullptr;
+    lp.shpre = L.has_shpre ? (const DevShadowCull*)(base + L.off_shpre) : nullptr;
     lp.n_clus = L.n_clus;
     lp.S = L.S, lp.P = L.P, lp.L = L.L, lp.limit = L.limit;
     lp.lights_a2_ok = L.lights_a2_ok ? 1 : 0;
@@ -1154,6 +1156,48 @@ double cell_hi(int k, float s, float o) {  // the highest x that can map to k (e
 float down(double v) { float f = (float)v; return (double)f > v ? std::nextafter(f, -INFINITY) : f; }
 float up(double v) { float f = (float)v; return (double)f < v ? std::nextafter(f, INFINITY) : f; }
 
+// The direct kernel's shadow pre-test records (rt_kernel.hip shadow_pre_keep; culling only).  The kernel drops
+// sphere i for a lane's shadow ray toward light l only under shadow_sphere_cull's rules for a single ray (R = 0)
+// from the lane's hit point O: w = C - O in the light's frame, margin 2^-8 dc + 2^-18 |O| with dc >= |C - O|,
+// line miss if w_u^2 + w_v^2 > (r' + 2^-18 |C| + margin)^2, behind if -w_a > margin.  Here dc is bounded by
+// |O_f|_1 + |C_f|_1 (frame coordinates), so the margin splits into a lane part m_l = 2^-8 (1 + 2^-8) |O_f|_1 +
+// 2^-30 (kernel: it also covers the 2^-18 |O| projection allowance, and its 2^-30 floor makes every cull imply
+// |C - O| > 2^-30) and a sphere part m_c = 2^-8 (1 + 2^-20) |C_f|_1, folded in here: ca' = ca + m_c and
+// rr' = r' + 2^-18 |C| + m_c, both rounded up.  Records that allow no culling -- a light whose a = p.p is outside
+// [2^-40, 2^40] or whose 2a is not finite, a sphere without a usable cull radius (NaN, < 2^-50), |C_f|_1 >= 2^38
+// or non-finite -- get ca' = rr' = +inf (no rule can hold); the padding sphere of an odd count gets cu = +inf
+// (always dropped: it never hits).
+void build_shadow_pre(const DevLight* li, int n_lights, const DevSphereCull* cull, int n_spheres, int s_pad,
+                      DevShadowCull* out) {
+    for (int j = 0; j < n_lights; ++j) {
+        const DevLight& d = li[j];
+        const bool l_ok = d.a >= 0x1p-40f && d.a <= 0x1p40f && d.a2 > 0.0f && d.a2 < INFINITY;
+        for (int i = 0; i < s_pad; ++i) {
+            DevShadowCull& e = out[(size_t)j * (size_t)s_pad + (size_t)i];
+            if (i >= n_spheres) {
+                e = DevShadowCull{INFINITY, 0.0f, 0.0f, 0.0f};
+                continue;
+            }
+            const double c[3] = {cull[i].cx, cull[i].cy, cull[i].cz};
+            const double clen = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+            const double cu = c[0] * d.ux + c[1] * d.uy + c[2] * d.uz;
+            const double cv = c[0] * d.vx + c[1] * d.vy + c[2] * d.vz;
+            const double ca = c[0] * d.ax + c[1] * d.ay + c[2] * d.az;
+            const double l1 = std::fabs((double)(float)cu) + std::fabs((double)(float)cv) + std::fabs((double)(float)ca);
+            const double mc = 0x1p-8 * l1 * (1.0 + 0x1p-20);
+            const bool ok = l_ok && cull[i].rr >= 0x1p-50f && l1 < 0x1p38 && std::isfinite(cull[i].rr) && std::isfinite(clen);
+            if (!ok) {
+                e = DevShadowCull{0.0f, 0.0f, INFINITY, INFINITY};
+                continue;
+            }
+            e.cu = (float)cu;
+            e.cv = (float)cv;
+            e.ca = std::nextafter((float)((double)(float)ca + mc), INFINITY);
+            e.rr = std::nextafter((float)((double)cull[i].rr + 0x1p-18 * clen + mc), INFINITY);
+        }
+    }
+}
+
 // Shadow grid of one light (DevShadowGrid; culling only -- a sphere left out of a lane's mask must
 // provably not block that lane's shadow ray in binary32).  The argument (rt_kernel.hip cull_mask):
 // IntersectsSphere yields disc < 0 when the exact line-to-centre distance D >= r (1 + 3 eps) +
@@ -1374,7 +1418,11 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
     int csize = CLUSTER_SIZE;
     if (const char* cv = std::getenv("RT_TRACE_CLUSTERS")) csize = std::atoi(cv);
     const bool want_clus = n_spheres >= CULL_MIN_SPHERES && n_spheres <= 64 && csize >= 1;
-    L.bytes = al(L.off_clus + (want_clus ? sizeof(DevCluster) * MAX_CLUSTERS : 0)) + 256;
+    L.off_shpre = al(L.off_clus + (want_clus ? sizeof(DevCluster) * MAX_CLUSTERS : 0));
+    // the direct kernel's shadow pre-test (S < CULL_MIN_SPHERES); RT_SHADOW_PRE=0 turns it off (A/B)
+    const char* pv = std::getenv("RT_SHADOW_PRE");
+    L.has_shpre = n_spheres < CULL_MIN_SPHERES && n_lights >= 1 && !(pv && std::strcmp(pv, "0") == 0);
+    L.bytes = al(L.off_shpre + (L.has_shpre ? sizeof(DevShadowCull) * (size_t)n_lights * (size_t)s_pad : 0)) + 256;
 
     std::vector<unsigned char> blob(L.bytes, 0);
     DevSphere* sph = (DevSphere*)(blob.data() + L.off_sph);
@@ -1457,6 +1505,7 @@ int rt_set_scene(rt_ctx* ctx, const rt_sphere* spheres, int n_spheres, const rt_
                 e.rr = std::nextafter((float)((double)cull[i].rr + 0x1p-18 * clen), INFINITY);
             }
     }
+    if (L.has_shpre) build_shadow_pre(li, n_lights, cull, n_spheres, s_pad, (DevShadowCull*)(blob.data() + L.off_shpre));
     for (int i = 0; i < n_spheres + n_planes; ++i)
         if ((mat[i].flags & MAT_SPEC) && mat[i].pow_kind == POW_GENERIC) L.generic_pow = true;
     for (Device& d : ctx->dev) {

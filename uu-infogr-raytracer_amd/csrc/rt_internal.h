@@ -88,6 +88,9 @@ struct DevShadowCull {
     float cu, cv, ca, rr;
 };
 constexpr long long SHADOW_CULL_MAX_ENTRIES = 1LL << 16;
+// The direct kernel's per-lane shadow pre-test (S < CULL_MIN_SPHERES; culling only): per (light, sphere) the
+// centre's (u, v) in the light's frame and, with the sphere's share of the margin folded in, the axial bound
+// ca' and the radius bound rr' (rt_api.cpp, rt_kernel.hip shadow_pre_keep).  Same record type, [L][S + (S & 1)].
 
 // Per-light shadow grid (bundle kernel's merged shadow pass, S <= 64 spheres, L <= 4 lights;
 // culling only).  Every shadow ray of light l has direction p_l, so whether sphere j can block a
@@ -167,6 +170,7 @@ struct LaunchParams {
     const DevLight* li;
     const DevSphereCull* scull;  // [S]
     const DevShadowCull* shcull;  // [L][S] or NULL (no shadow culling)
+    const DevShadowCull* shpre;   // [L][S + (S & 1)] the direct kernel's shadow pre-test, or NULL
     const DevShadowGrid* shg;     // [L] or NULL (no shadow grid: the per-level bound instead)
     const unsigned long long* shgrid;  // [L][SHGRID_N^2]
     const unsigned long long* shslab;  // [L][SHGRID_SLABS + 2]
