@@ -18,7 +18,9 @@ make -s -C $C obj/rt_api.o obj/rt_codec.o >/dev/null 2>&1 || make -C $C $C/obj/r
 F="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -fno-fast-math -fhip-fp32-correctly-rounded-divide-sqrt -fno-gpu-flush-denormals-to-zero"
 /opt/rocm/bin/hipcc $F -fno-slp-vectorize "$@" -I$R/include -c -o $T/k.o $T/x/csrc/rt_kernel.hip
 API=$C/obj/rt_api.o
-if ! cmp -s $C/rt_api.cpp $T/x/csrc/rt_api.cpp; then
+changed=0
+for f in rt_api.cpp $(cd $C && ls *.h); do cmp -s $C/$f $T/x/csrc/$f || changed=1; done
+if [ $changed = 1 ]; then  # rt_api.cpp or a header it includes (record layouts) changed
     /opt/rocm/bin/hipcc $F "$@" -x hip -c -o $T/api.o $T/x/csrc/rt_api.cpp
     API=$T/api.o
 fi

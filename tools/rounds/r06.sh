@@ -110,5 +110,11 @@ j)  # the GPU suite on the product (direct kernel's shadow pre-test), then wall 
     echo "gpu tests: $(tail -1 $O/gpu_j.log)"
     bash tools/ab_wall.sh "${CFGS:-C3 C2 C1 REF}" lib/probe/libraytracer_hip_nopre.so lib/libraytracer_hip.so | tee $O/ab_pre_product.txt
     ;;
+k)  # the GPU suite on the product, then the parity subset and wall per frame of probe builds LIBS against it
+    timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/gpu_k.log 2>&1 \
+        || { echo "GPU TESTS FAILED"; tail -30 $O/gpu_k.log; exit 1; }
+    echo "gpu tests: $(tail -1 $O/gpu_k.log)"
+    bash $0 i
+    ;;
 *)  echo "unknown step $1"; exit 2 ;;
 esac
