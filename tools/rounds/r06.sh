@@ -116,5 +116,10 @@ k)  # the GPU suite on the product, then the parity subset and wall per frame of
     echo "gpu tests: $(tail -1 $O/gpu_k.log)"
     bash $0 i
     ;;
+l)  # timing-only ablation builds (wrong pixels: no parity), wall per frame against the product: LIBS, CFGS, TAG
+    args=""
+    for n in $LIBS; do args="$args lib/probe/libraytracer_hip_$n.so"; done
+    bash tools/ab_wall.sh "$CFGS" $args lib/libraytracer_hip.so | tee $O/ab_${TAG:-l}.txt
+    ;;
 *)  echo "unknown step $1"; exit 2 ;;
 esac
